@@ -1,0 +1,202 @@
+"""Benchmark: DPVO update iterations/s (altcorr + fastba) on the BASELINE cfg2
+synthetic patch graph -- 96 patches x 2048 edges, p=3, 4-level pyramid
+[1,2,4,8], fp32 -- on N MI355X GPUs (replicas; one process per GPU).
+
+One step = one DPVO update iteration with all inputs resident in HBM:
+  F-REPROJ  (cuda_ba.reproject, E x 9 points)
+  A-CORR    (all 4 levels in one launch, cuda_corr.forward_levels)
+  F-BA      (cuda_ba.forward, 2 iterations, poses/patches updated in place)
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "update-iterations/sec (altcorr+fastba) on 96-patch/2048-edge graph, 1→8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def algorithmic_corr_bytes(coords, H2s, W2s, scales, C, p, R, feat_bytes):
+    """per edge per level
+    B_l = s_f C p^2 (gmap patch) + s_f C U_l (fmap window union) + 2 p^2 4 (coords)
+          + 16 (ii, jj) + (2R+1)^2 p^2 4 (output, fp32)
+    with U_l = number of distinct in-map fmap pixels touched by the edge's p^2
+    windows at level l, computed exactly from the coordinates."""
+    import torch
+
+    D = 2 * R + 2
+    E = coords.shape[1]
+    off = torch.arange(D, device=coords.device) - R
+    total = 0
+    per_level = []
+    for H2, W2, s in zip(H2s, W2s, scales):
+        c = coords[0] / s  # [E, 2, p, p]
+        x0 = c[:, 0].floor().long().view(E, -1)  # [E, p*p]
+        y0 = c[:, 1].floor().long().view(E, -1)
+        xs = (x0[:, :, None, None] + off.view(1, 1, 1, D)).expand(E, p * p, D, D)
+        ys = (y0[:, :, None, None] + off.view(1, 1, D, 1)).expand(E, p * p, D, D)
+        inb = (xs >= 0) & (xs < W2) & (ys >= 0) & (ys < H2)
+        key = torch.where(inb, ys * W2 + xs, torch.full_like(xs, -1)).reshape(E, -1)
+        key, _ = key.sort(dim=1)
+        distinct = ((key[:, 1:] != key[:, :-1]) & (key[:, 1:] >= 0)).sum(1) + (key[:, 0] >= 0).long()
+        U = distinct.sum().item()
+        b = E * (feat_bytes * C * p * p + 2 * p * p * 4 + 16 + (2 * R + 1) ** 2 * p * p * 4)
+        b += feat_bytes * C * U
+        per_level.append({"scale": s, "U_mean": U / E, "bytes": b})
+        total += b
+    return total, per_level
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--levels", default="1,2,4,8")
+    ap.add_argument("--ba-iters", type=int, default=2)
+    ap.add_argument("--mem", type=int, default=36, help="feature ring-buffer frames (DPVO mem)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from dpvo_amd import altcorr, fastba, synthetic
+
+    levels = [int(x) for x in args.levels.split(",")]
+    G = synthetic.make_config(args.config, seed=args.seed)  # same graph on every rank (replicas)
+    D = G.to(dev)
+    P = G.patches.shape[-1]
+    C = 128
+    pyr = synthetic.make_features(mem=args.mem, C=C, levels=levels, seed=args.seed, device=dev)
+    # gmap: patch features of every (frame, slot), DPVO's pmem = mem ring
+    gbuf = torch.zeros(1, args.mem * G.M, C, P, P, device=dev)
+    centres = D.patches[: G.F * G.M, :2, P // 2, P // 2]  # [F*M, 2] (x, y)
+    for f in range(G.F):
+        gbuf[0, f * G.M:(f + 1) * G.M] = altcorr.patchify(
+            pyr[0][:, f], centres[f * G.M:(f + 1) * G.M].unsqueeze(0), P // 2)[0]
+    lmbda = torch.tensor([1e-4], device=dev)
+    poses, patches = D.poses.clone(), D.patches.clone()
+    kk1 = D.kk % (G.M * args.mem)  # dpvo.py:456-457
+    jj1 = D.jj % args.mem
+    scales = [float(s) for s in levels]
+
+    ev_corr = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+
+    def step(i=None):
+        coords = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk)
+        if i is not None:
+            ev_corr[i][0].record()
+        corr = altcorr.corr_levels(gbuf, pyr, coords, kk1, jj1, 3, scales)
+        if i is not None:
+            ev_corr[i][1].record()
+        fastba.BA(poses, patches, D.intrinsics, D.target, D.weight, lmbda, D.ii, D.jj, D.kk, 1,
+                  G.F, M=G.M, iterations=args.ba_iters)
+        return corr
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    coords0 = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk)
+    alg_bytes, per_level = algorithmic_corr_bytes(
+        coords0, [f.shape[3] for f in pyr], [f.shape[4] for f in pyr], scales, C, P, 3, 4)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    corr_ms = sum(a.elapsed_time(b) for a, b in ev_corr) / args.steps
+
+    if world > 1:
+        t = torch.tensor([elapsed, corr_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, corr_ms = t[0].item(), t[1].item()
+
+    value = world * args.steps / elapsed
+    achieved = alg_bytes / (corr_ms * 1e-3) / 1e9  # GB/s of the dominant kernel
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import cpu_baseline  # baseline infrastructure (CPU port of the reference path)
+
+        threads = min(16, os.cpu_count() or 1)
+        ips, thr, n = cpu_baseline.measure(G, levels=tuple(levels), budget_s=args.cpu_budget,
+                                           threads=threads, mem=args.mem, C=C)
+        cpu = {"value": ips, "unit": "update-iterations/s", "cores": thr, "kind": "port",
+               "sample": f"{n} full {args.config} update iteration(s) (reproject + "
+                         f"{len(levels)}-level grid_sample corr + {args.ba_iters} ba.py BA "
+                         f"steps), torch CPU, {thr} threads"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "update-iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (SURVEY 8d cfg2 recipe, seeded)",
+            "config": {
+                "workload": f"{args.config}: {G.M} patches/frame x {G.E} edges, p={P}, "
+                            f"{len(levels)}-level pyramid {levels}, fp32, BA {args.ba_iters} iters",
+                "patches_per_frame": G.M, "edges": G.E, "frames": G.F, "levels": levels,
+                "radius": 3, "channels": C, "feature_ring": args.mem,
+                "parallelism": f"replicas x{world}",
+            },
+            "roofline": {
+                "kernel": "corr_fwd_levels_kernel (A-CORR, all levels, one launch)",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "kernel_ms": corr_ms,
+                "per_level": per_level,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

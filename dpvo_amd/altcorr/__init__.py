@@ -1,0 +1,15 @@
+"""altcorr on MI355X: patch correlation (A-CORR) and patch extraction (A-PATCH).
+
+Same entry points as dpvo/altcorr/correlation.py of cuteboyqq/DPVO
+(`corr`, `patchify`, `CorrLayer`, `PatchLayer`), backed by the `cuda_corr`
+HIP extension.  Extra: `corr_levels`, the fused all-levels call of
+DPVO.corr (dpvo/dpvo.py:456-465) in one launch.
+"""
+from .correlation import (  # noqa: F401
+    BORDER_MODE,
+    CorrLayer,
+    PatchLayer,
+    corr,
+    corr_levels,
+    patchify,
+)

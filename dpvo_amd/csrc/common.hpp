@@ -1,0 +1,180 @@
+// common.hpp -- shared device/host helpers for the gfx950 DPVO hot path.
+#pragma once
+
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dpvo_hot.h"
+
+#define DPVO_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace dpvo {
+
+constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? DPVO_OK : DPVO_ERR_LAUNCH;
+}
+
+// --- element type helpers ---------------------------------------------------
+template <typename T>
+struct Acc { using type = float; };
+template <>
+struct Acc<double> { using type = double; };
+
+__device__ __forceinline__ float to_acc(float v) { return v; }
+__device__ __forceinline__ float to_acc(__half v) { return __half2float(v); }
+__device__ __forceinline__ double to_acc(double v) { return v; }
+
+template <typename T>
+__device__ __forceinline__ T from_acc(float v);
+template <>
+__device__ __forceinline__ float from_acc<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ __half from_acc<__half>(float v) { return __float2half(v); }
+template <>
+__device__ __forceinline__ double from_acc<double>(float v) { return (double)v; }
+__device__ __forceinline__ double from_acc_d(double v) { return v; }
+
+// static_cast<int>(floor(v)) with out-of-range values pushed far outside
+// every map (the reference is undefined there; correlation_kernel.cu:156-157)
+__device__ __forceinline__ int ifloor_safe(float v) {
+  float f = floorf(v);
+  f = fminf(fmaxf(f, -1.0e8f), 1.0e8f);  // NaN -> -1e8 (fmaxf drops NaN)
+  return (int)f;
+}
+
+__device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Order LDS traffic between lanes of ONE wave (a wave's DS ops execute in
+// order; this stops the compiler from moving them across the point).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// --- fp32 SE3 primitives of ba_cuda.cu:36-174 (restated, device) ---------------
+__device__ __forceinline__ void actSO3(const float* q, const float* X, float* Y) {
+  float uv[3];
+  uv[0] = 2.0f * (q[1] * X[2] - q[2] * X[1]);
+  uv[1] = 2.0f * (q[2] * X[0] - q[0] * X[2]);
+  uv[2] = 2.0f * (q[0] * X[1] - q[1] * X[0]);
+  Y[0] = X[0] + q[3] * uv[0] + (q[1] * uv[2] - q[2] * uv[1]);
+  Y[1] = X[1] + q[3] * uv[1] + (q[2] * uv[0] - q[0] * uv[2]);
+  Y[2] = X[2] + q[3] * uv[2] + (q[0] * uv[1] - q[1] * uv[0]);
+}
+
+__device__ __forceinline__ void actSE3(const float* t, const float* q, const float* X, float* Y) {
+  actSO3(q, X, Y);
+  Y[3] = X[3];
+  Y[0] += X[3] * t[0];
+  Y[1] += X[3] * t[1];
+  Y[2] += X[3] * t[2];
+}
+
+// Ji = Adj(Gij)^T Jj (ba_cuda.cu:57-72)
+__device__ __forceinline__ void adjSE3(const float* t, const float* q, const float* X, float* Y) {
+  float qinv[4] = {-q[0], -q[1], -q[2], q[3]};
+  actSO3(qinv, &X[0], &Y[0]);
+  actSO3(qinv, &X[3], &Y[3]);
+  float u[3], v[3];
+  u[0] = t[2] * X[1] - t[1] * X[2];
+  u[1] = t[0] * X[2] - t[2] * X[0];
+  u[2] = t[1] * X[0] - t[0] * X[1];
+  actSO3(qinv, u, v);
+  Y[3] += v[0];
+  Y[4] += v[1];
+  Y[5] += v[2];
+}
+
+// Gij = Pj * Pi^-1 (ba_cuda.cu:74-85)
+__device__ __forceinline__ void relSE3(const float* ti, const float* qi, const float* tj,
+                                       const float* qj, float* tij, float* qij) {
+  qij[0] = -qj[3] * qi[0] + qj[0] * qi[3] - qj[1] * qi[2] + qj[2] * qi[1];
+  qij[1] = -qj[3] * qi[1] + qj[1] * qi[3] - qj[2] * qi[0] + qj[0] * qi[2];
+  qij[2] = -qj[3] * qi[2] + qj[2] * qi[3] - qj[0] * qi[1] + qj[1] * qi[0];
+  qij[3] = qj[3] * qi[3] + qj[0] * qi[0] + qj[1] * qi[1] + qj[2] * qi[2];
+  actSO3(qij, ti, tij);
+  tij[0] = tj[0] - tij[0];
+  tij[1] = tj[1] - tij[1];
+  tij[2] = tj[2] - tij[2];
+}
+
+__device__ __forceinline__ void expSO3(const float* phi, float* q) {  // ba_cuda.cu:88-110
+  float theta_sq = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+  float theta_p4 = theta_sq * theta_sq;
+  float theta = sqrtf(theta_sq);
+  float imag, real;
+  if (theta_sq < 1e-8f) {
+    imag = 0.5f - (1.0f / 48.0f) * theta_sq + (1.0f / 3840.0f) * theta_p4;
+    real = 1.0f - (1.0f / 8.0f) * theta_sq + (1.0f / 384.0f) * theta_p4;
+  } else {
+    imag = sinf(0.5f * theta) / theta;
+    real = cosf(0.5f * theta);
+  }
+  q[0] = imag * phi[0];
+  q[1] = imag * phi[1];
+  q[2] = imag * phi[2];
+  q[3] = real;
+}
+
+__device__ __forceinline__ void crossInplace(const float* a, float* b) {
+  float x0 = a[1] * b[2] - a[2] * b[1];
+  float x1 = a[2] * b[0] - a[0] * b[2];
+  float x2 = a[0] * b[1] - a[1] * b[0];
+  b[0] = x0;
+  b[1] = x1;
+  b[2] = x2;
+}
+
+__device__ __forceinline__ void expSE3(const float* xi, float* t, float* q) {  // :125-153
+  expSO3(xi + 3, q);
+  float tau[3] = {xi[0], xi[1], xi[2]};
+  float phi[3] = {xi[3], xi[4], xi[5]};
+  float theta_sq = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+  float theta = sqrtf(theta_sq);
+  t[0] = tau[0];
+  t[1] = tau[1];
+  t[2] = tau[2];
+  if (theta > 1e-4f) {
+    float a = (1.0f - cosf(theta)) / theta_sq;
+    crossInplace(phi, tau);
+    t[0] += a * tau[0];
+    t[1] += a * tau[1];
+    t[2] += a * tau[2];
+    float b = (theta - sinf(theta)) / (theta * theta_sq);
+    crossInplace(phi, tau);
+    t[0] += b * tau[0];
+    t[1] += b * tau[1];
+    t[2] += b * tau[2];
+  }
+}
+
+// pose <- Exp(xi) * pose, no renormalisation (ba_cuda.cu:156-174)
+__device__ __forceinline__ void retrSE3(const float* xi, const float* t, const float* q, float* t1,
+                                        float* q1) {
+  float dt[3] = {0, 0, 0};
+  float dq[4] = {0, 0, 0, 1};
+  expSE3(xi, dt, dq);
+  q1[0] = dq[3] * q[0] + dq[0] * q[3] + dq[1] * q[2] - dq[2] * q[1];
+  q1[1] = dq[3] * q[1] + dq[1] * q[3] + dq[2] * q[0] - dq[0] * q[2];
+  q1[2] = dq[3] * q[2] + dq[2] * q[3] + dq[0] * q[1] - dq[1] * q[0];
+  q1[3] = dq[3] * q[3] - dq[0] * q[0] - dq[1] * q[1] - dq[2] * q[2];
+  actSO3(dq, t, t1);
+  t1[0] += dt[0];
+  t1[1] += dt[1];
+  t1[2] += dt[2];
+}
+
+}  // namespace dpvo

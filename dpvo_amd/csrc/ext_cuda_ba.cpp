@@ -1,0 +1,189 @@
+// ext_cuda_ba.cpp -- the `cuda_ba` extension module (drop-in for
+// dpvo/fastba/ba.cpp:183-189), bound to the C ABI in dpvo_hot.h.
+#include "ext_common.hpp"
+
+using namespace dpvo_ext;
+
+static torch::Tensor f32_contig(const torch::Tensor& t, const char* name) {
+  check_device(t, name);
+  // packed_accessor32<float> in the reference (ba_cuda.cu:496-501) rejects
+  // other dtypes with a RuntimeError; keep that behaviour.
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32, got ",
+              t.scalar_type());
+  return t.contiguous();
+}
+
+// ba.cpp:32-45 -> cuda_ba (ba_cuda.cu:433-582).  Mutates poses / patches.
+std::vector<torch::Tensor> ba_forward(torch::Tensor poses, torch::Tensor patches,
+                                      torch::Tensor intrinsics, torch::Tensor target,
+                                      torch::Tensor weight, torch::Tensor lmbda, torch::Tensor ii,
+                                      torch::Tensor jj, torch::Tensor kk, int PPF, int t0, int t1,
+                                      int iterations, bool eff_impl) {
+  check_device(poses, "poses");
+  check_device(patches, "patches");
+  TORCH_CHECK(poses.scalar_type() == torch::kFloat32 && patches.scalar_type() == torch::kFloat32,
+              "poses / patches must be float32");
+  // poses.view({-1,7}) / patches.view({-1,3,P,P}) must alias the caller's
+  // storage for the in-place update to land (ba_cuda.cu:458-459)
+  TORCH_CHECK(poses.is_contiguous() && patches.is_contiguous(),
+              "poses and patches must be contiguous (updated in place)");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  const int P = patches.size(-1);
+  const int num_poses = poses.numel() / 7;
+  const int num_patches = patches.numel() / (3 * P * P);
+  intrinsics = f32_contig(intrinsics, "intrinsics");
+  target = f32_contig(target, "target");
+  weight = f32_contig(weight, "weight");
+  lmbda = f32_contig(lmbda, "lmbda");
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  kk = idx64(kk, "kk");
+  const int E = ii.numel();
+  TORCH_CHECK(jj.numel() == E && kk.numel() == E, "ii, jj, kk must have equal length");
+  TORCH_CHECK(target.numel() >= 2 * E && weight.numel() >= 2 * E, "target/weight must be [.., E, 2]");
+  if (E == 0 || iterations <= 0) return {};
+  TORCH_CHECK(t1 - t0 <= dpvo_ba_max_free_poses(), "cuda_ba.forward: t1 - t0 = ", t1 - t0,
+              " free poses exceeds this build's single-workgroup Schur solve (",
+              dpvo_ba_max_free_poses(), ")");
+  const size_t wsb = dpvo_ba_workspace_bytes(E, t0, t1);
+  auto ws = torch::empty({(int64_t)wsb}, poses.options().dtype(torch::kUInt8));
+  check_status(dpvo_ba_forward(poses.data_ptr<float>(), patches.data_ptr<float>(),
+                               intrinsics.data_ptr<float>(), target.data_ptr<float>(),
+                               weight.data_ptr<float>(), lmbda.data_ptr<float>(),
+                               ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(),
+                               kk.data_ptr<int64_t>(), E, P, num_poses, num_patches, PPF, t0, t1,
+                               iterations, eff_impl ? 1 : 0, ws.data_ptr(), wsb,
+                               current_stream()),
+               "cuda_ba.forward");
+  return {};
+}
+
+// ba.cpp:47-53 -> cuda_reproject (ba_cuda.cu:585-616)
+torch::Tensor ba_reproject(torch::Tensor poses, torch::Tensor patches, torch::Tensor intrinsics,
+                           torch::Tensor ii, torch::Tensor jj, torch::Tensor kk) {
+  poses = f32_contig(poses, "poses");
+  patches = f32_contig(patches, "patches");
+  intrinsics = f32_contig(intrinsics, "intrinsics");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  kk = idx64(kk, "kk");
+  const int P = patches.size(-1);
+  const int E = ii.numel();
+  auto coords = torch::empty({E, 2, P, P}, poses.options());
+  check_status(dpvo_reproject(poses.data_ptr<float>(), patches.data_ptr<float>(),
+                              intrinsics.data_ptr<float>(), ii.data_ptr<int64_t>(),
+                              jj.data_ptr<int64_t>(), kk.data_ptr<int64_t>(), E, P,
+                              poses.numel() / 7, patches.numel() / (3 * P * P),
+                              coords.data_ptr<float>(), current_stream()),
+               "cuda_ba.reproject");
+  return coords.view({1, E, 2, P, P});
+}
+
+// ba.cpp:59-97 (host loop in the reference; here one O(E^2) LDS-tiled kernel)
+std::vector<torch::Tensor> ba_neighbors(torch::Tensor ii, torch::Tensor jj) {
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ii.device());
+  const int E = ii.numel();
+  auto ix = torch::empty({E}, ii.options());
+  auto jx = torch::empty({E}, ii.options());
+  check_status(dpvo_neighbors(ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), E,
+                              ix.data_ptr<int64_t>(), jx.data_ptr<int64_t>(), current_stream()),
+               "cuda_ba.neighbors");
+  return {ix, jx};
+}
+
+// ba.cpp:120-180: Sim3 pose-graph solve of the loop-closure backend.
+std::vector<torch::Tensor> ba_solve_system(torch::Tensor, torch::Tensor, torch::Tensor,
+                                           torch::Tensor, torch::Tensor, double, double, int) {
+  TORCH_CHECK(false,
+              "cuda_ba.solve_system (loop-closure pose graph, dpvo/fastba/ba.cpp:120-180) is not "
+              "part of this build (SURVEY 8f rank 2)");
+  return {};
+}
+
+// Split F-BA for the edge-sharded multi-GPU path.
+torch::Tensor ba_setup(torch::Tensor ii, torch::Tensor jj, torch::Tensor kk, int num_patches,
+                       int t0, int t1) {
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  kk = idx64(kk, "kk");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ii.device());
+  const int E = ii.numel();
+  const size_t wsb = dpvo_ba_workspace_bytes(E, t0, t1);
+  auto ws = torch::empty({(int64_t)wsb}, ii.options().dtype(torch::kUInt8));
+  check_status(dpvo_ba_setup(ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(),
+                             kk.data_ptr<int64_t>(), E, num_patches, t0, t1, ws.data_ptr(), wsb,
+                             current_stream()),
+               "cuda_ba.setup");
+  return ws;
+}
+
+std::vector<torch::Tensor> ba_build_schur(torch::Tensor ws, torch::Tensor poses,
+                                          torch::Tensor patches, torch::Tensor intrinsics,
+                                          torch::Tensor target, torch::Tensor weight,
+                                          torch::Tensor lmbda, torch::Tensor ii, torch::Tensor jj,
+                                          torch::Tensor kk, int t0, int t1) {
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  TORCH_CHECK(poses.is_contiguous() && patches.is_contiguous(), "poses/patches contiguous");
+  intrinsics = f32_contig(intrinsics, "intrinsics");
+  target = f32_contig(target, "target");
+  weight = f32_contig(weight, "weight");
+  lmbda = f32_contig(lmbda, "lmbda");
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  kk = idx64(kk, "kk");
+  const int N = t1 - t0, E = ii.numel(), P = patches.size(-1);
+  auto S = torch::zeros({N * (N + 1) / 2, 6, 6}, poses.options().dtype(torch::kFloat64));
+  auto y = torch::zeros({6 * N}, poses.options().dtype(torch::kFloat64));
+  check_status(dpvo_ba_build_schur(poses.data_ptr<float>(), patches.data_ptr<float>(),
+                                   intrinsics.data_ptr<float>(), target.data_ptr<float>(),
+                                   weight.data_ptr<float>(), lmbda.data_ptr<float>(),
+                                   ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(),
+                                   kk.data_ptr<int64_t>(), E, P, poses.numel() / 7, t0, t1,
+                                   ws.data_ptr(), S.data_ptr<double>(), y.data_ptr<double>(),
+                                   current_stream()),
+               "cuda_ba.build_schur");
+  return {S, y};
+}
+
+torch::Tensor ba_solve_update(torch::Tensor ws, torch::Tensor poses, torch::Tensor patches,
+                              torch::Tensor S, torch::Tensor y, int E, int t0, int t1) {
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  TORCH_CHECK(poses.is_contiguous() && patches.is_contiguous(), "poses/patches contiguous");
+  S = S.contiguous();
+  y = y.contiguous();
+  TORCH_CHECK(S.scalar_type() == torch::kFloat64 && y.scalar_type() == torch::kFloat64,
+              "S / y must be float64");
+  const int N = t1 - t0, P = patches.size(-1);
+  auto dX = torch::zeros({N > 0 ? N : 0, 6}, poses.options().dtype(torch::kFloat64));
+  check_status(dpvo_ba_solve_update(poses.data_ptr<float>(), patches.data_ptr<float>(),
+                                    S.data_ptr<double>(), y.data_ptr<double>(), E, P,
+                                    poses.numel() / 7, t0, t1, ws.data_ptr(),
+                                    N > 0 ? dX.data_ptr<double>() : nullptr, current_stream()),
+               "cuda_ba.solve_update");
+  return dX;
+}
+
+torch::Tensor ba_last_status(torch::Tensor ws, int E, int t0, int t1) {
+  auto out = torch::zeros({1}, ws.options().dtype(torch::kInt32));
+  check_status(dpvo_ba_last_status(ws.data_ptr(), E, t0, t1, out.data_ptr<int>(),
+                                   current_stream()),
+               "cuda_ba.last_status");
+  return out;
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("forward", &ba_forward, "BA forward operator");
+  m.def("neighbors", &ba_neighbors, "temporal neighboor indicies");
+  m.def("reproject", &ba_reproject, "temporal neighboor indicies");
+  m.def("solve_system", &ba_solve_system, "temporal neighboor indicies");
+  // additions: split BA for the sharded multi-GPU path
+  m.def("setup", &ba_setup, "BA graph setup -> workspace");
+  m.def("build_schur", &ba_build_schur, "linearize + Schur complement (S_lower, y)");
+  m.def("solve_update", &ba_solve_update, "Cholesky solve + pose/patch retraction");
+  m.def("last_status", &ba_last_status, "status word of the last BA on a workspace");
+  m.def("max_free_poses", &dpvo_ba_max_free_poses);
+  m.attr("native_library") = dpvo_version();
+}

@@ -1,0 +1,172 @@
+// ext_cuda_corr.cpp -- the `cuda_corr` extension module (drop-in for
+// dpvo/altcorr/correlation.cpp:57-63), bound to the C ABI in dpvo_hot.h.
+#include "ext_common.hpp"
+
+using namespace dpvo_ext;
+
+// correlation.cpp:32-38 -> correlation_kernel.cu:232-272
+std::vector<torch::Tensor> corr_forward(torch::Tensor fmap1, torch::Tensor fmap2,
+                                        torch::Tensor coords, torch::Tensor ii, torch::Tensor jj,
+                                        int radius) {
+  check_device(fmap1, "fmap1");
+  check_device(fmap2, "fmap2");
+  check_device(coords, "coords");
+  TORCH_CHECK(fmap1.dim() == 5 && fmap2.dim() == 5 && coords.dim() == 5,
+              "corr: expected fmap1 [B,N1,C,H,W], fmap2 [B,N2,C,H2,W2], coords [B,M,2,H,W]");
+  TORCH_CHECK(fmap1.scalar_type() == fmap2.scalar_type(), "fmap1/fmap2 dtype mismatch");
+  TORCH_CHECK(coords.scalar_type() == torch::kFloat32, "coords must be float32");
+  TORCH_CHECK(coords.size(2) == 2, "coords must be [B,M,2,H,W]");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(fmap1.device());
+  fmap1 = fmap1.contiguous();
+  fmap2 = fmap2.contiguous();
+  coords = coords.contiguous();
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  const int B = coords.size(0), M = coords.size(1), H = coords.size(3), W = coords.size(4);
+  TORCH_CHECK(ii.numel() >= M && jj.numel() >= M, "ii/jj shorter than coords.size(1)");
+  TORCH_CHECK(fmap1.size(3) == H && fmap1.size(4) == W, "fmap1 patch size != coords size");
+  const int Dp = 2 * radius + 1;
+  auto out = torch::empty({B, M, Dp, Dp, H, W}, fmap1.options());
+  check_status(dpvo_corr_forward(fmap1.data_ptr(), fmap2.data_ptr(), coords.data_ptr<float>(),
+                                 ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), B, M,
+                                 fmap1.size(2), H, W, fmap1.size(1), fmap2.size(1), fmap2.size(3),
+                                 fmap2.size(4), radius, dtype_code(fmap1), out.data_ptr(),
+                                 current_stream()),
+               "cuda_corr.forward");
+  return {out};
+}
+
+// Fused multi-level form (dpvo/dpvo.py:462-465): returns [B, M, Dp, Dp, H, W, L]
+// float32 = torch.stack([corr(level l) for l], -1).
+torch::Tensor corr_forward_levels(torch::Tensor fmap1, std::vector<torch::Tensor> fmap2,
+                                  torch::Tensor coords, torch::Tensor ii, torch::Tensor jj,
+                                  int radius, std::vector<double> scales) {
+  check_device(fmap1, "fmap1");
+  TORCH_CHECK(fmap2.size() == scales.size() && !fmap2.empty() && fmap2.size() <= 8,
+              "one scale per pyramid level (1..8 levels)");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(fmap1.device());
+  fmap1 = fmap1.contiguous();
+  coords = coords.contiguous();
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  TORCH_CHECK(coords.scalar_type() == torch::kFloat32 && coords.dim() == 5, "coords [B,M,2,H,W] f32");
+  const int L = fmap2.size();
+  std::vector<const void*> ptrs(L);
+  std::vector<int> H2(L), W2(L);
+  std::vector<float> sc(L);
+  for (int l = 0; l < L; l++) {
+    check_device(fmap2[l], "fmap2");
+    TORCH_CHECK(fmap2[l].scalar_type() == fmap1.scalar_type(), "fmap dtype mismatch");
+    fmap2[l] = fmap2[l].contiguous();
+    ptrs[l] = fmap2[l].data_ptr();
+    H2[l] = fmap2[l].size(3);
+    W2[l] = fmap2[l].size(4);
+    sc[l] = (float)scales[l];
+  }
+  const int B = coords.size(0), M = coords.size(1), H = coords.size(3), W = coords.size(4);
+  const int Dp = 2 * radius + 1;
+  auto out = torch::empty({B, M, Dp, Dp, H, W, L}, fmap1.options().dtype(torch::kFloat32));
+  check_status(dpvo_corr_forward_levels(fmap1.data_ptr(), ptrs.data(), H2.data(), W2.data(),
+                                        sc.data(), L, coords.data_ptr<float>(),
+                                        ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), B, M,
+                                        fmap1.size(2), H, W, fmap1.size(1), fmap2[0].size(1),
+                                        radius, dtype_code(fmap1), out.data_ptr<float>(),
+                                        current_stream()),
+               "cuda_corr.forward_levels");
+  return out;
+}
+
+// correlation.cpp:40-48 -> correlation_kernel.cu:275-325
+std::vector<torch::Tensor> corr_backward(torch::Tensor fmap1, torch::Tensor fmap2,
+                                         torch::Tensor coords, torch::Tensor ii, torch::Tensor jj,
+                                         torch::Tensor corr_grad, int radius) {
+  check_device(fmap1, "fmap1");
+  check_device(corr_grad, "corr_grad");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(fmap1.device());
+  const auto dtype = fmap1.scalar_type();
+  // the atomic accumulation runs in fp32 for every input dtype
+  auto f1 = fmap1.to(torch::kFloat32).contiguous();
+  auto f2 = fmap2.to(torch::kFloat32).contiguous();
+  coords = coords.to(torch::kFloat32).contiguous();
+  auto g = corr_grad.to(torch::kFloat32).contiguous();
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  const int B = coords.size(0), M = coords.size(1), H = coords.size(3), W = coords.size(4);
+  auto g1 = torch::empty_like(f1);
+  auto g2 = torch::empty_like(f2);
+  check_status(dpvo_corr_backward(f1.data_ptr(), f2.data_ptr(), coords.data_ptr<float>(),
+                                  ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(),
+                                  g.data_ptr<float>(), B, M, f1.size(2), H, W, f1.size(1),
+                                  f2.size(1), f2.size(3), f2.size(4), radius, DPVO_F32,
+                                  g1.data_ptr(), g2.data_ptr(), current_stream()),
+               "cuda_corr.backward");
+  return {g1.to(dtype), g2.to(dtype)};
+}
+
+static std::vector<torch::Tensor> patchify_fwd_impl(torch::Tensor net, torch::Tensor coords,
+                                                    int radius, bool clamp) {
+  check_device(net, "net");
+  check_device(coords, "coords");
+  TORCH_CHECK(net.dim() == 4 && coords.dim() == 3 && coords.size(2) == 2,
+              "patchify: expected net [B,C,H,W], coords [B,M,2]");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(net.device());
+  net = net.contiguous();
+  coords = coords.to(torch::kFloat32).contiguous();
+  const int B = coords.size(0), M = coords.size(1), C = net.size(1), D = 2 * radius + 2;
+  auto out = torch::empty({B, M, C, D, D}, net.options());
+  check_status(dpvo_patchify_forward(net.data_ptr(), coords.data_ptr<float>(), B, C, net.size(2),
+                                     net.size(3), M, radius, clamp ? 1 : 0, dtype_code(net),
+                                     out.data_ptr(), current_stream()),
+               "cuda_corr.patchify_forward");
+  return {out};
+}
+
+// correlation.cpp:50-53 -> correlation_kernel.cu:327-346 (zero fill)
+std::vector<torch::Tensor> patchify_forward(torch::Tensor net, torch::Tensor coords, int radius) {
+  return patchify_fwd_impl(net, coords, radius, false);
+}
+// The fork's runtime patchify (clamp at the border), correlation_kernel.py:181-224
+std::vector<torch::Tensor> patchify_forward_clamped(torch::Tensor net, torch::Tensor coords,
+                                                    int radius) {
+  return patchify_fwd_impl(net, coords, radius, true);
+}
+
+static std::vector<torch::Tensor> patchify_bwd_impl(torch::Tensor net, torch::Tensor coords,
+                                                    torch::Tensor gradient, int radius,
+                                                    bool clamp) {
+  check_device(net, "net");
+  check_device(gradient, "gradient");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(net.device());
+  coords = coords.to(torch::kFloat32).contiguous();
+  auto g = gradient.to(torch::kFloat32).contiguous();
+  const int B = coords.size(0), M = coords.size(1), C = net.size(1);
+  auto out = torch::empty({net.size(0), C, net.size(2), net.size(3)},
+                          net.options().dtype(torch::kFloat32));
+  check_status(dpvo_patchify_backward(g.data_ptr(), coords.data_ptr<float>(), B, C, net.size(2),
+                                      net.size(3), M, radius, clamp ? 1 : 0, DPVO_F32,
+                                      out.data_ptr(), current_stream()),
+               "cuda_corr.patchify_backward");
+  return {out.to(net.scalar_type())};
+}
+
+// correlation.cpp:55-58 -> correlation_kernel.cu:349-372
+std::vector<torch::Tensor> patchify_backward(torch::Tensor net, torch::Tensor coords,
+                                             torch::Tensor gradient, int radius) {
+  return patchify_bwd_impl(net, coords, gradient, radius, false);
+}
+std::vector<torch::Tensor> patchify_backward_clamped(torch::Tensor net, torch::Tensor coords,
+                                                     torch::Tensor gradient, int radius) {
+  return patchify_bwd_impl(net, coords, gradient, radius, true);
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("forward", &corr_forward, "CORR forward");
+  m.def("backward", &corr_backward, "CORR backward");
+  m.def("patchify_forward", &patchify_forward, "PATCHIFY forward");
+  m.def("patchify_backward", &patchify_backward, "PATCHIFY backward");
+  // additions (not in the reference surface)
+  m.def("forward_levels", &corr_forward_levels, "CORR forward, all pyramid levels in one launch");
+  m.def("patchify_forward_clamped", &patchify_forward_clamped, "PATCHIFY forward, border clamp");
+  m.def("patchify_backward_clamped", &patchify_backward_clamped, "PATCHIFY backward, border clamp");
+  m.attr("native_library") = dpvo_version();
+}

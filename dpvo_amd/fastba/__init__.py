@@ -1,0 +1,38 @@
+"""fastba on MI355X: Schur bundle adjustment (F-BA), reprojection (F-REPROJ)
+and edge neighbours (F-NBR), backed by the `cuda_ba` HIP extension.
+
+Reference surface: dpvo/fastba/ba.py:1-8 (cuteboyqq/DPVO) --
+`BA(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1,
+M, iterations, eff_impl=False)` updates poses[t0:t1] and the inverse depth
+of every patch in kk IN PLACE and returns nothing useful (the extension
+returns []); `neighbors(ii, jj)`; `reproject(poses, patches, intrinsics,
+ii, jj, kk)` -> [1, E, 2, P, P].
+"""
+from __future__ import annotations
+
+from .._native import load_extension
+
+cuda_ba = load_extension("cuda_ba")
+
+
+def BA(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, M, iterations,
+       eff_impl=False):
+    """fastba.BA (dpvo/fastba/ba.py:7-8): note the extension's argument order
+    puts patches-per-frame (M) before t0 (ba.cpp:32-45)."""
+    data = poses.data if hasattr(poses, "data") else poses
+    return cuda_ba.forward(data, patches, intrinsics, target, weight, lmbda, ii, jj, kk, M, t0, t1,
+                           iterations, eff_impl)
+
+
+def neighbors(ii, jj):
+    """cuda_ba.neighbors (ba.cpp:59-97): previous / next edge of the same ii
+    ordered by jj (stable), -1 at the ends."""
+    return cuda_ba.neighbors(ii, jj)
+
+
+def reproject(poses, patches, intrinsics, ii, jj, kk):
+    """cuda_ba.reproject (ba_cuda.cu:379-429, 585-616)."""
+    return cuda_ba.reproject(poses, patches, intrinsics, ii, jj, kk)
+
+
+__all__ = ["BA", "neighbors", "reproject", "cuda_ba"]

@@ -1,0 +1,183 @@
+/*
+ * dpvo_hot.h -- C ABI of the MI355X (gfx950) DPVO hot path.
+ *
+ * Every entry point takes plain device pointers, sizes and an opaque HIP
+ * stream (`void*`, hipStream_t; NULL = legacy default stream), launches
+ * hand-written HIP kernels on that stream and returns a dpvo_status.  No
+ * entry point allocates device memory, synchronises or copies to the host,
+ * so each call is hipGraph-capturable; scratch memory is passed in as a
+ * caller-owned workspace sized by the matching *_workspace_bytes().
+ *
+ * Each function names the reference interface it replaces (paths relative to
+ * /root/reference, cuteboyqq/DPVO).  The Python extension modules cuda_corr,
+ * cuda_ba and lietorch_backends (dpvo_amd/csrc/ext_*.cpp) bind exactly these.
+ *
+ * Layouts (row-major, contiguous):
+ *   fmap1   [B, N1, C, H, W]    gmap patch features (H = W = p)
+ *   fmap2   [B, N2, C, H2, W2]  one pyramid level of frame features
+ *   coords  [B, M, 2, H, W]     float32 (x, y) per patch pixel, this level
+ *   ii, jj  [M]                 int64 patch / frame index per edge
+ *   corr    [B, M, 2R+1, 2R+1, H, W]  axis 2 = x offset, axis 3 = y offset
+ *   poses   [*, 7]  float32 (tx, ty, tz, qx, qy, qz, qw)
+ *   patches [*, 3, P, P] float32 (x, y, inverse depth)
+ */
+#ifndef DPVO_HOT_H
+#define DPVO_HOT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  DPVO_OK = 0,
+  DPVO_ERR_INVALID = 1,     /* bad argument (shape, dtype, null pointer)      */
+  DPVO_ERR_LAUNCH = 2,      /* hipLaunchKernel / hipGetLastError failure       */
+  DPVO_ERR_UNSUPPORTED = 3, /* configuration outside what this build handles   */
+  DPVO_ERR_WORKSPACE = 4    /* workspace smaller than *_workspace_bytes()      */
+} dpvo_status;
+
+typedef enum { DPVO_F32 = 0, DPVO_F16 = 1, DPVO_F64 = 2 } dpvo_dtype;
+
+/* Human-readable text for a status code (static storage). */
+const char* dpvo_status_string(int status);
+/* Build identification, e.g. "dpvo_hot gfx950 <git>". */
+const char* dpvo_version(void);
+
+/* ---------------------------------------------------------------- altcorr */
+
+/* A-CORR.  Replaces cuda_corr.forward (dpvo/altcorr/correlation.cpp:57,
+   correlation_kernel.cu:232-272 + corr_forward_kernel :82-175).
+   out[B,M,2R+1,2R+1,H,W] in fmap dtype; accumulation is always fp32 (f64 for
+   DPVO_F64).  Requires H*W <= 16, R <= 7. */
+int dpvo_corr_forward(const void* fmap1, const void* fmap2, const float* coords,
+                      const int64_t* ii, const int64_t* jj, int B, int M, int C, int H, int W,
+                      int N1, int N2, int H2, int W2, int radius, int dtype, void* out,
+                      void* stream);
+
+/* A-CORR, all pyramid levels of one DPVO update in one launch (the fused form
+   of the two/four per-level calls at dpvo/dpvo.py:462-465).  fmap2[l] is
+   [B, N2, C, H2[l], W2[l]]; coords are level-1 coordinates and are divided by
+   scale[l] in-kernel (dpvo.py:462-463 passes coords / 1 and coords / 4).
+   out is [B, M, 2R+1, 2R+1, H, W, L] float = DPVO's torch.stack(..., -1). */
+int dpvo_corr_forward_levels(const void* fmap1, const void* const* fmap2, const int* H2,
+                             const int* W2, const float* scale, int L, const float* coords,
+                             const int64_t* ii, const int64_t* jj, int B, int M, int C, int H,
+                             int W, int N1, int N2, int radius, int dtype, float* out,
+                             void* stream);
+
+/* A-CORR-BWD.  Replaces cuda_corr.backward (correlation.cpp:58,
+   correlation_kernel.cu:275-325 + corr_backward_kernel :178-229).
+   grad [B,M,2R+1,2R+1,H,W] float32.  fmap1_grad / fmap2_grad are ZEROED by
+   this call and then accumulated (fp32 atomics, like the reference). */
+int dpvo_corr_backward(const void* fmap1, const void* fmap2, const float* coords,
+                       const int64_t* ii, const int64_t* jj, const float* grad, int B, int M,
+                       int C, int H, int W, int N1, int N2, int H2, int W2, int radius, int dtype,
+                       void* fmap1_grad, void* fmap2_grad, void* stream);
+
+/* A-PATCH.  Replaces cuda_corr.patchify_forward (correlation.cpp:60,
+   correlation_kernel.cu:327-346 + patchify_forward_kernel :16-47).
+   net [B,C,H,W], coords [B,M,2] float32 -> out [B,M,C,D,D], D = 2R+2.
+   clamp=0: zero fill outside the map (CUDA semantics); clamp=1: clamp to the
+   border (the fork's runtime patchify_forward_kernel_python,
+   correlation_kernel.py:181-224). */
+int dpvo_patchify_forward(const void* net, const float* coords, int B, int C, int H, int W, int M,
+                          int radius, int clamp, int dtype, void* out, void* stream);
+
+/* A-PATCH-BWD.  Replaces cuda_corr.patchify_backward (correlation.cpp:61,
+   correlation_kernel.cu:349-372 + patchify_backward_kernel :49-80).
+   net_grad [B,C,H,W] is zeroed by this call, then scatter-added. */
+int dpvo_patchify_backward(const void* grad, const float* coords, int B, int C, int H, int W,
+                           int M, int radius, int clamp, int dtype, void* net_grad, void* stream);
+
+/* ---------------------------------------------------------------- fastba */
+
+/* Workspace for dpvo_ba_forward / the split BA entry points. */
+size_t dpvo_ba_workspace_bytes(int E, int t0, int t1);
+
+/* Largest number of free poses (t1 - t0) the single-workgroup Schur solve
+   handles in this build. */
+int dpvo_ba_max_free_poses(void);
+
+/* F-BA.  Replaces cuda_ba.forward (dpvo/fastba/ba.cpp:32-45 -> cuda_ba,
+   ba_cuda.cu:433-582; fastba.BA, dpvo/fastba/ba.py:7-8).  Runs `iterations`
+   Gauss-Newton/Schur steps and updates poses[t0:t1] and the inverse depth of
+   every patch kk[*] IN PLACE.  lmbda is a device pointer to one float.
+   eff_impl / PPF select the reference's block-sparse E (block_e.cu); this
+   implementation is block-sparse for every call and accepts both values.
+   Reductions and the Cholesky solve are fp64, deterministic (no float
+   atomics).  A failed factorisation yields dX = 0 and status flag bit 1 in
+   ws-reported diagnostics (dpvo_ba_last_status). */
+int dpvo_ba_forward(float* poses, float* patches, const float* intrinsics, const float* target,
+                    const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
+                    const int64_t* kk, int E, int P, int num_poses, int num_patches, int PPF,
+                    int t0, int t1, int iterations, int eff_impl, void* workspace,
+                    size_t workspace_bytes, void* stream);
+
+/* Split form of dpvo_ba_forward used by the edge-sharded multi-GPU BA
+   (SURVEY 8e): setup once per call, then per iteration build the local Schur
+   system, all-reduce (S, y) across ranks, and solve+update.
+   S_lower: [N(N+1)/2][6][6] double (block (a,b), a >= b, row-major blocks in
+   order a*(a+1)/2 + b); y: [6N] double. */
+int dpvo_ba_setup(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
+                  int t0, int t1, void* workspace, size_t workspace_bytes, void* stream);
+int dpvo_ba_build_schur(const float* poses, const float* patches, const float* intrinsics,
+                        const float* target, const float* weight, const float* lmbda,
+                        const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int P,
+                        int num_poses, int t0, int t1, void* workspace, double* S_lower,
+                        double* y, void* stream);
+int dpvo_ba_solve_update(float* poses, float* patches, const double* S_lower, const double* y,
+                         int E, int P, int num_poses, int t0, int t1, void* workspace,
+                         double* dX_out, void* stream);
+/* Status word of the last BA call on this workspace, copied to the DEVICE int
+   `out`: bit 0 = Cholesky failed in the last solve (dX was set to 0),
+   bit 1 = some kk outside [0, num_patches) (clamped). */
+int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1, int* out, void* stream);
+
+/* F-REPROJ.  Replaces cuda_ba.reproject (ba.cpp:47-53 -> cuda_reproject,
+   ba_cuda.cu:585-616 + reproject :379-429).  coords [E,2,P,P]. */
+int dpvo_reproject(const float* poses, const float* patches, const float* intrinsics,
+                   const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int P,
+                   int num_poses, int num_patches, float* coords, void* stream);
+
+/* F-NBR.  Replaces cuda_ba.neighbors (ba.cpp:59-97).  Groups edges by ii,
+   stable-sorts each group by jj; ix = previous edge, jx = next edge, -1 at
+   the ends.  Single-workgroup LDS sort: E <= dpvo_neighbors_max_edges(). */
+int dpvo_neighbors_max_edges(void);
+int dpvo_neighbors(const int64_t* ii, const int64_t* jj, int E, int64_t* ix, int64_t* jx,
+                   void* stream);
+
+/* ---------------------------------------------------------------- lietorch */
+
+/* L-SE3.  Replaces lietorch_backends.{expm, logm, inv, mul, adj, adjT, act,
+   act4, as_matrix, projector, Jinv} (dpvo/lietorch/src/lietorch.cpp:18-283,
+   lietorch_gpu.cu:20-601).  group: 1 = SO3, 3 = SE3 (dispatch.h:24-45).
+   dtype DPVO_F32 / DPVO_F64.  n elements, each row contiguous:
+     op 0 exp   : X=a[K]          -> out[N]
+     op 1 log   : X[N]            -> out[K]
+     op 2 inv   : X[N]            -> out[N]
+     op 3 mul   : X[N], Y[N]      -> out[N]
+     op 4 adj   : X[N], Y=a[K]    -> out[K]
+     op 5 adjT  : X[N], Y=a[K]    -> out[K]
+     op 6 act   : X[N], Y=p[3]    -> out[3]
+     op 7 act4  : X[N], Y=p[4]    -> out[4]
+     op 8 matrix: X[N]            -> out[4x4]
+     op 9 proj  : X[N]            -> out[NxN]
+     op 10 Jinv : X[N], Y=a[K]    -> out[K]
+   Quaternions are normalised on load (so3.h:95-97). */
+int dpvo_lie_forward(int group, int op, int dtype, int n, const void* X, const void* Y, void* out,
+                     void* stream);
+
+/* Backward of ops 0-7 (lietorch_gpu.cu:32-256); gradient rows of group
+   elements are N-strided with the tangent gradient in the first K entries
+   (the reference convention).  out0 = dX (or da for exp), out1 = dY/da/dp. */
+int dpvo_lie_backward(int group, int op, int dtype, int n, const void* grad, const void* X,
+                      const void* Y, void* out0, void* out1, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DPVO_HOT_H */

@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprofv3 kernel trace.
+# Stops at the first crash / timeout (exit 124/134/137/139); plain test
+# failures (exit 1) still let the later steps run.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+fatal() { case "$1" in 124|134|137|139|-6|-11) return 0;; *) return 1;; esac; }
+STEPS="${STEPS:-tests smoke bench prof}"
+for s in $STEPS; do
+  case $s in
+    tests) timeout -k 10 900 python -m pytest tests -m gpu -q -rf > $OUT/pytest_gpu.log 2>&1; rc=$?;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?;;
+    bench) timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; rc=$?;;
+    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline > $OUT/prof.log 2>&1; rc=$?;;
+    *) echo "unknown step $s"; rc=0;;
+  esac
+  echo "step $s rc=$rc"
+  tail -3 $OUT/*$s*.log 2>/dev/null | tail -3
+  if fatal $rc; then echo "fatal rc=$rc at $s; stopping"; exit $rc; fi
+done
+exit 0

@@ -1,0 +1,188 @@
+"""GPU parity of altcorr (A-CORR, A-CORR-BWD, A-PATCH, A-PATCH-BWD) through the
+cuda_corr extension (-> C ABI -> HIP kernels) against the reference's golden
+vectors and the oracle.
+
+Tolerances (fp32): the reference accumulates the 128-long dot in fp32 in an
+arbitrary order, the oracle in fp64; elementwise |gpu - ref| <= 1e-5 *
+max(1, |ref|_max) covers fp32 summation noise (north_star: "fp32 correlation
+volumes within 1e-4 rel")."""
+import numpy as np
+import pytest
+import torch
+from conftest import golden
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cc(gpu):
+    import dpvo_amd
+
+    return dpvo_amd.load_extension("cuda_corr")
+
+
+def _t(a, dev, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return t.to(dtype) if dtype is not None else t
+
+
+def _close(out, ref, tol=1e-5):
+    ref = np.asarray(ref, np.float64)
+    out = np.asarray(out, np.float64)
+    assert out.shape == ref.shape
+    err = np.abs(out - ref).max() if ref.size else 0.0
+    assert err <= tol * max(1.0, np.abs(ref).max() if ref.size else 1.0), err
+
+
+@pytest.mark.parametrize("name", ["corr_loop_a", "corr_loop_b", "corr_loop_c", "corr_gs_a"])
+def test_forward_matches_reference_golden(cc, gpu, name):
+    z = golden(name)
+    out, = cc.forward(_t(z["fmap1"], gpu), _t(z["fmap2"], gpu), _t(z["coords"], gpu),
+                      _t(z["ii"], gpu), _t(z["jj"], gpu), int(z["radius"]))
+    _close(out.cpu().numpy(), z["out"], 1e-5 if name != "corr_gs_a" else 2e-5)
+
+
+def _case(seed, B=1, M=37, C=128, N1=9, N2=4, H2=24, W2=32, p=3, R=3, spread=0.3, far=0.1,
+          Hp=None, Wp=None):
+    r = np.random.default_rng(seed)
+    Hp = Hp or p
+    Wp = Wp or p
+    f1 = (0.25 * r.standard_normal((B, N1, C, Hp, Wp))).astype(np.float32)
+    f2 = (0.25 * r.standard_normal((B, N2, C, H2, W2))).astype(np.float32)
+    cx = r.uniform(-4, W2 + 4, (B, M, 1, 1))
+    cy = r.uniform(-4, H2 + 4, (B, M, 1, 1))
+    gx = np.arange(Wp)[None, None, None, :] - Wp // 2 + spread * r.standard_normal((B, M, Hp, Wp))
+    gy = np.arange(Hp)[None, None, :, None] - Hp // 2 + spread * r.standard_normal((B, M, Hp, Wp))
+    co = np.stack([cx + gx, cy + gy], 2).astype(np.float32)
+    co[:, : int(far * M), 0] += 5 * W2  # windows completely outside the map
+    ii = r.integers(0, N1, M)
+    jj = r.integers(0, N2, M)
+    return f1, f2, co, ii, jj, R
+
+
+@pytest.mark.parametrize("kw", [
+    dict(),                                  # DPVO shape: p=3, R=3, C=128
+    dict(R=0), dict(R=1), dict(R=2), dict(R=7),
+    dict(p=1), dict(p=2), dict(p=4),         # other exact patch sizes
+    dict(Hp=2, Wp=3),                        # non-square patch -> generic path
+    dict(spread=4.0),                        # windows too spread for the box
+    dict(B=2, M=11),                         # batch
+    dict(C=37, M=5),                         # channel tail (C % 4 != 0)
+    dict(H2=5, W2=6, M=21),                  # tiny map: every window clipped
+])
+def test_forward_matches_oracle(cc, gpu, kw):
+    f1, f2, co, ii, jj, R = _case(1, **kw)
+    out, = cc.forward(_t(f1, gpu), _t(f2, gpu), _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R)
+    _close(out.cpu().numpy(), oracle.corr_fwd(f1, f2, co, ii, jj, R))
+
+
+def test_forward_cfg2_full_size(cc, gpu):
+    # full BASELINE cfg2 edge count against the oracle (both levels of DPVO.corr)
+    from dpvo_amd import synthetic
+
+    G = synthetic.make_config("cfg2", seed=0)
+    pyr = synthetic.make_features(mem=12, levels=(1, 4), seed=0, device=gpu)
+    r = np.random.default_rng(0)
+    gmap = (0.25 * r.standard_normal((1, 12 * 96, 128, 3, 3))).astype(np.float32)
+    coords = oracle.reproject(G.poses.numpy(), G.patches.numpy(), G.intrinsics.numpy(),
+                              G.ii.numpy(), G.jj.numpy(), G.kk.numpy())
+    for lvl, s in enumerate((1, 4)):
+        co = (coords / s).astype(np.float32)
+        f2 = pyr[lvl].cpu().numpy()
+        out, = cc.forward(_t(gmap, gpu), pyr[lvl], _t(co, gpu), _t(G.kk.numpy(), gpu),
+                          _t(G.jj.numpy(), gpu), 3)
+        _close(out.cpu().numpy(), oracle.corr_fwd(gmap, f2, co, G.kk.numpy(), G.jj.numpy(), 3))
+
+
+def test_forward_is_deterministic(cc, gpu):
+    f1, f2, co, ii, jj, R = _case(2, M=200)
+    args = (_t(f1, gpu), _t(f2, gpu), _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R)
+    a, = cc.forward(*args)
+    b, = cc.forward(*args)
+    assert torch.equal(a, b)
+
+
+def test_forward_levels_equals_per_level_calls(cc, gpu):
+    from dpvo_amd import altcorr
+
+    f1, f2, co, ii, jj, R = _case(3, M=64, H2=40, W2=48)
+    f1, co, ii, jj = _t(f1, gpu), _t(co, gpu), _t(ii, gpu), _t(jj, gpu)
+    lv1 = _t(f2, gpu)
+    lv2 = torch.nn.functional.avg_pool2d(lv1[0], 4, 4).unsqueeze(0).contiguous()
+    fused = altcorr.corr_levels(f1, [lv1, lv2], co, ii, jj, R, scales=(1, 4))
+    c1, = cc.forward(f1, lv1, co / 1, ii, jj, R)
+    c2, = cc.forward(f1, lv2, co / 4, ii, jj, R)
+    ref = torch.stack([c1, c2], -1).view(1, len(ii), -1)  # dpvo.py:465
+    assert torch.equal(fused, ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float64])
+def test_forward_other_dtypes(cc, gpu, dtype):
+    f1, f2, co, ii, jj, R = _case(4, M=23)
+    f1h, f2h = torch.from_numpy(f1).to(dtype), torch.from_numpy(f2).to(dtype)
+    out, = cc.forward(f1h.to(gpu), f2h.to(gpu), _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R)
+    assert out.dtype == dtype
+    ref = oracle.corr_fwd(f1h.double().numpy(), f2h.double().numpy(), co, ii, jj, R)
+    _close(out.double().cpu().numpy(), ref, 2e-3 if dtype == torch.float16 else 1e-6)
+
+
+def test_forward_empty(cc, gpu):
+    f1, f2, co, ii, jj, R = _case(5, M=3)
+    out, = cc.forward(_t(f1, gpu), _t(f2, gpu), _t(co[:, :0], gpu), _t(ii[:0], gpu),
+                      _t(jj[:0], gpu), R)
+    assert out.shape == (1, 0, 7, 7, 3, 3)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(spread=4.0), dict(R=1, M=9)])
+def test_backward_matches_oracle(cc, gpu, kw):
+    f1, f2, co, ii, jj, R = _case(6, M=19, C=32, **kw)
+    Dp = 2 * R + 1
+    G = np.random.default_rng(7).standard_normal((1, len(ii), Dp, Dp, 3, 3)).astype(np.float32)
+    g1, g2 = cc.backward(_t(f1, gpu), _t(f2, gpu), _t(co, gpu), _t(ii, gpu), _t(jj, gpu),
+                         _t(G, gpu), R)
+    r1, r2 = oracle.corr_bwd(f1, f2, co, ii, jj, G, R)
+    _close(g1.cpu().numpy(), r1, 1e-5)
+    _close(g2.cpu().numpy(), r2, 1e-5)
+
+
+@pytest.mark.parametrize("name", ["patchify_a", "patchify_b", "patchify_c"])
+def test_patchify_matches_reference_golden(cc, gpu, name):
+    z = golden(name)
+    R = int(z["radius"])
+    net, co = _t(z["net"], gpu), _t(z["coords"], gpu)
+    zero, = cc.patchify_forward(net, co, R)
+    clamp, = cc.patchify_forward_clamped(net, co, R)
+    np.testing.assert_array_equal(zero.cpu().numpy(), z["out_zero"])
+    np.testing.assert_array_equal(clamp.cpu().numpy(), z["out_clamp"])
+
+
+@pytest.mark.parametrize("clamp", [False, True])
+def test_patchify_backward_matches_oracle(cc, gpu, clamp):
+    r = np.random.default_rng(8)
+    net = r.standard_normal((1, 16, 20, 24)).astype(np.float32)
+    co = np.stack([r.uniform(-3, 27, (1, 40)), r.uniform(-3, 23, (1, 40))], -1).astype(np.float32)
+    G = r.standard_normal((1, 40, 16, 4, 4)).astype(np.float32)
+    fn = cc.patchify_backward_clamped if clamp else cc.patchify_backward
+    g, = fn(_t(net, gpu), _t(co, gpu), _t(G, gpu), 1)
+    _close(g.cpu().numpy(), oracle.patchify_bwd(net.shape, co, G, 1, clamp), 1e-5)
+
+
+def test_autograd_wrappers(gpu):
+    # dpvo_amd.altcorr mirrors dpvo/altcorr/correlation.py (CorrLayer / PatchLayer)
+    from dpvo_amd import altcorr
+
+    f1, f2, co, ii, jj, R = _case(9, M=12, C=16)
+    a = _t(f1, gpu).requires_grad_()
+    b = _t(f2, gpu).requires_grad_()
+    out = altcorr.corr(a, b, _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R)
+    G = torch.randn_like(out)
+    (out * G).sum().backward()
+    r1, r2 = oracle.corr_bwd(f1, f2, co, ii, jj, G.cpu().numpy(), R)
+    _close(a.grad.cpu().numpy(), r1)
+    _close(b.grad.cpu().numpy(), r2)
+    net = torch.randn(1, 8, 20, 20, device=gpu)
+    c2 = torch.rand(1, 10, 2, device=gpu) * 18 + 1
+    p = altcorr.patchify(net, c2, 1)
+    assert p.shape == (1, 10, 8, 3, 3)
