@@ -36,7 +36,7 @@ struct BaWs {
   int32_t* boff;    // [E+1] patch -> pose-block range
   int32_t* bpose;   // [2E]  free pose of each block (ascending per patch)
   int32_t* eslot;   // [2E]  block slot of (ii, jj) of each edge, -1 = fixed pose
-  int32_t* meta;    // [4]   nuniq, status, nblocks
+  int32_t* meta;    // [4]   nuniq, status, nblocks, num_patches
   int64_t* kx;      // [E]   unique patch ids (ascending)
   int64_t* skey;    // [E]   sorted kk (scratch)
   float* J;         // [E][32]
@@ -192,6 +192,7 @@ __global__ void __launch_bounds__(kSetupThreads)
     w.poff[nuniq] = E;
     w.meta[0] = nuniq;
     w.meta[1] = bad ? 2 : 0;
+    w.meta[3] = num_patches;
   }
   __syncthreads();
   // ---- per-patch free-pose lists (N <= 32: one bit per free pose) ----
@@ -315,8 +316,9 @@ __global__ void __launch_bounds__(256)
     ix = min(max(ix, 0), num_poses - 1);  // memory guard (reference: unchecked)
     jx = min(max(jx, 0), num_poses - 1);
     float* o = w.J + (size_t)kJStride * e;
+    const int64_t kx = min(max(kk[e], (int64_t)0), (int64_t)w.meta[3] - 1);
     edge_linearize(poses, patches, P, fx, fy, cx, cy, target[2 * e], target[2 * e + 1],
-                   weight[2 * e], weight[2 * e + 1], ix, jx, kk[e], o);
+                   weight[2 * e], weight[2 * e + 1], ix, jx, kx, o);
     const int si = w.eslot[2 * e], sj = w.eslot[2 * e + 1];
     for (int row = 0; row < 2; row++) {
       const double wr = o[row];
