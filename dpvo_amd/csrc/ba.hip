@@ -6,46 +6,77 @@
 //   Q = 1/(C+lmbda); S = B - E Q E^T; y = v - E Q u; S += I*(1e-4 S + 1)
 //   dX = chol_solve(S, y); dZ = Q (u - E^T dX); pose / patch retraction.
 //
-// MI355X design (DESIGN.md "F-BA"): no float atomics anywhere.
-//   setup  (1 WG, once per call): sort kk in LDS (bitonic), unique/inverse,
-//          group edges by patch, build each patch's sorted free-pose list.
-//   linearize (thread per patch): the fp32 edge math of the reference, patch
-//          sums C,u and the patch's E column blocks c_{u,p} (fp64, private).
-//   schur  (one WG per lower 6x6 block of S): B and E Q E^T terms reduced in
-//          registers + LDS in a fixed order -> deterministic fp64 S, y.
-//   solve  (1 WG): damping, fp64 Cholesky in LDS (L kept in the upper
-//          triangle, one barrier per column), triangular solves in one wave,
-//          pose retraction, dZ and patch retraction.
-// The split (build_schur -> all-reduce(S,y) -> solve_update) is the
-// edge-sharded multi-GPU form.
+// MI355X design (DESIGN.md "F-BA").  A DPVO window is small (N <= 20 free
+// poses, a few thousand edges) and the reference spends its time in ~15
+// kernel launches, float atomics and a host-side Cholesky per iteration.
+// Here the whole BA call -- setup and every iteration -- is ONE workgroup of
+// 1024 threads on one CU, phases separated by barriers, no float atomics,
+// every reduction in a fixed order (bitwise deterministic):
+//   setup      sort kk in LDS (bitonic), unique/inverse, edges grouped by
+//              patch, per-patch free-pose bitmask + block offsets, per-pose
+//              edge lists and patch lists (counts matrix + one block scan).
+//   linearize  thread per edge: the fp32 edge math of the reference
+//              -> J (fp32) and the edge's E/C/u contributions (fp64).
+//   patch      thread per patch: Q_u, U_u and the E column blocks c_{u,p}.
+//   schur      gather, one team of lanes per lower 6x6 block of S: the team
+//              walks only the edge/patch lists of its pose, reduces in
+//              registers + shuffles; S and y land in LDS.
+//   solve      damping, right-looking block Cholesky in LDS (6x6 diagonal
+//              blocks factored + inverted by one lane, look-ahead so the
+//              factor overlaps the trailing update), block substitutions
+//              in one wave.
+//   update     pose retraction, dZ = Q (u - E^T dX), patch retraction.
+// The split (build_schur -> all-reduce(S,y) -> solve_update) runs the same
+// phases in three single-workgroup kernels: the edge-sharded multi-GPU form
+// (SURVEY 8e).
 #include "common.hpp"
 
 namespace dpvo {
 
-constexpr int kSetupThreads = 1024;
-constexpr int kMaxSetupE = 16384;  // LDS: 16384 x 8 B keys = 128 KiB
-constexpr int kMaxFree = 20;       // 6N <= 120: fp64 S in LDS = 116 KiB (and <= 32 for masks)
-constexpr int kSchurThreads = 256;
-constexpr int kSolveThreads = 1024;
-constexpr int kJStride = 32;       // floats per edge: w r Jz Ji[2][6] Jj[2][6]
+constexpr int kBaThreads = 1024;
+constexpr int kMaxSetupE = 16384;  // LDS: 16384 x 8 B sort keys = 128 KiB
+constexpr int kMaxFree = 20;       // lower blocks of S for N=20: 59 KiB of LDS
+constexpr int kPerThread = kMaxSetupE / kBaThreads;
+constexpr int kJStride = 32;       // floats per edge: w[2] r[2] Jz[2] Ji[2][6] Jj[2][6]
+constexpr int kEStride = 16;       // doubles per edge: Ei[6] Ej[6] C u
+constexpr int kCtlBytes = 512;     // LDS control words + scan scratch
+constexpr int kNoPose = 31;        // "other pose" code of an edge with one free end
+constexpr int kMarks = 32;         // start, setup, then 5 phases x up to 6 iterations
 
 struct BaWs {
-  int32_t* ku;      // [E]   inverse index into unique patches
-  int32_t* pedge;   // [E]   edges grouped by patch (ascending edge id)
+  int32_t* pedge;   // [E]   edges grouped by patch (ascending edge id within a patch)
   int32_t* poff;    // [E+1] patch -> edge range
   int32_t* boff;    // [E+1] patch -> pose-block range
   int32_t* bpose;   // [2E]  free pose of each block (ascending per patch)
-  int32_t* eslot;   // [2E]  block slot of (ii, jj) of each edge, -1 = fixed pose
-  int32_t* meta;    // [4]   nuniq, status, nblocks, num_patches
+  uint32_t* pmask;  // [E]   free poses touched by each patch
+  int32_t* eoff;    // [kMaxFree+1] pose -> range of elist
+  int32_t* elist;   // [2E]  per pose: (edge << 8) | (other pose << 2) | roles
+  int32_t* qoff;    // [kMaxFree+1] pose -> range of qlist
+  int32_t* qlist;   // [2E]  per pose: patches touching it
+  int32_t* meta;    // [8]   nuniq, status, nblocks, num_patches
   int64_t* kx;      // [E]   unique patch ids (ascending)
-  int64_t* skey;    // [E]   sorted kk (scratch)
   float* J;         // [E][32]
+  double* EC;       // [E][16]
   double* Q;        // [E]
   double* U;        // [E]
   double* cb;       // [2E][6]
-  double* S;        // [NL][36]
+  double* S;        // [NL][36] (split API default)
   double* y;        // [6N]
   double* dX;       // [6N]
+  int64_t* tmark;   // [kMarks] wall-clock marks of the fused kernel's phases
+};
+
+struct BaArgs {
+  float* poses;  // written in place; never restrict (read again after the update)
+  float* patches;
+  const float* intrinsics;
+  const float* target;
+  const float* weight;
+  const float* lmbda;
+  const int64_t* ii;
+  const int64_t* jj;
+  const int64_t* kk;
+  int E, P, num_poses, num_patches, t0, N;
 };
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
@@ -59,29 +90,52 @@ static size_t ba_layout(int E, int N, char* base, BaWs* w) {
     return p;
   };
   BaWs t;
-  t.ku = (int32_t*)take(sizeof(int32_t) * E);
   t.pedge = (int32_t*)take(sizeof(int32_t) * E);
   t.poff = (int32_t*)take(sizeof(int32_t) * (E + 1));
   t.boff = (int32_t*)take(sizeof(int32_t) * (E + 1));
   t.bpose = (int32_t*)take(sizeof(int32_t) * 2 * E);
-  t.eslot = (int32_t*)take(sizeof(int32_t) * 2 * E);
-  t.meta = (int32_t*)take(sizeof(int32_t) * 4);
+  t.pmask = (uint32_t*)take(sizeof(uint32_t) * E);
+  t.eoff = (int32_t*)take(sizeof(int32_t) * (kMaxFree + 1));
+  t.elist = (int32_t*)take(sizeof(int32_t) * 2 * E);
+  t.qoff = (int32_t*)take(sizeof(int32_t) * (kMaxFree + 1));
+  t.qlist = (int32_t*)take(sizeof(int32_t) * 2 * E);
+  t.meta = (int32_t*)take(sizeof(int32_t) * 8);
   t.kx = (int64_t*)take(sizeof(int64_t) * E);
-  t.skey = (int64_t*)take(sizeof(int64_t) * E);
   t.J = (float*)take(sizeof(float) * kJStride * E);
+  t.EC = (double*)take(sizeof(double) * kEStride * E);
   t.Q = (double*)take(sizeof(double) * E);
   t.U = (double*)take(sizeof(double) * E);
   t.cb = (double*)take(sizeof(double) * 12 * E);
   t.S = (double*)take(sizeof(double) * 36 * (NL ? NL : 1));
   t.y = (double*)take(sizeof(double) * 6 * (N ? N : 1));
   t.dX = (double*)take(sizeof(double) * 6 * (N ? N : 1));
+  t.tmark = (int64_t*)take(sizeof(int64_t) * kMarks);
   if (w) *w = t;
   return off;
 }
 
+// LDS bytes of each phase group (all LDS is dynamic, carved from one base).
+static size_t setup_lds(int P2, int N) {
+  const size_t ints = (size_t)(P2 > N * kBaThreads ? P2 : N * kBaThreads);
+  const size_t a = sizeof(unsigned long long) * (size_t)P2, b = sizeof(int) * ints;
+  return kCtlBytes + (a > b ? a : b);
+}
+static size_t solve_lds(int N) {
+  const size_t NL = (size_t)N * (N + 1) / 2;
+  return kCtlBytes + sizeof(double) * (36 * NL + 36 * (size_t)N + 6 * (size_t)N);
+}
+
+__device__ __forceinline__ int tri_row(int t) {  // a with a(a+1)/2 <= t < (a+1)(a+2)/2
+  int r = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+  while (r * (r + 1) / 2 > t) r--;
+  while ((r + 1) * (r + 2) / 2 <= t) r++;
+  return r;
+}
+__device__ __forceinline__ int blk(int a, int b) { return a * (a + 1) / 2 + b; }  // a >= b
+
 // ---------------------------------------------------------------------------
 // block-wide exclusive scan of data[0..n) in LDS (int), returns the total.
-// scratch: >= kSetupThreads/64 + 1 ints of LDS.
+// Callers barrier before (data complete); the scan ends with a barrier.
 // ---------------------------------------------------------------------------
 __device__ int block_exclusive_scan(int* data, int n, int* scratch) {
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -89,7 +143,6 @@ __device__ int block_exclusive_scan(int* data, int n, int* scratch) {
   const int lo = min(tid * per, n), hi = min(lo + per, n);
   int s = 0;
   for (int i = lo; i < hi; i++) s += data[i];
-  // inclusive wave scan of s
   const int lane = tid & 63, wid = tid >> 6;
   int v = s;
 #pragma unroll
@@ -109,7 +162,7 @@ __device__ int block_exclusive_scan(int* data, int n, int* scratch) {
     scratch[nt / 64] = acc;
   }
   __syncthreads();
-  int run = scratch[wid] + v - s;  // exclusive prefix of this thread's chunk
+  int run = scratch[wid] + v - s;
   for (int i = lo; i < hi; i++) {
     const int x = data[i];
     data[i] = run;
@@ -120,37 +173,37 @@ __device__ int block_exclusive_scan(int* data, int n, int* scratch) {
   return total;
 }
 
+__device__ __forceinline__ bool is_free(int64_t p, int N) { return p >= 0 && p < N; }
+
 // ---------------------------------------------------------------------------
-// setup: unique/inverse of kk (torch::_unique(kk, sorted, inverse),
-// ba_cuda.cu:447), edges grouped by patch, per-patch free-pose block lists.
+// SETUP: unique/inverse of kk (torch::_unique(kk, sorted, inverse),
+// ba_cuda.cu:447) and the sparse structure every later phase walks.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kSetupThreads)
-    ba_setup_kernel(const int64_t* __restrict__ ii, const int64_t* __restrict__ jj,
-                    const int64_t* __restrict__ kk, int E, int num_patches, int t0, int N,
-                    int P2, BaWs w) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long keys[];
-  const int tid = threadIdx.x, nt = blockDim.x;
-  int* scratch = reinterpret_cast<int*>(keys + P2);  // kSetupThreads/64 + 1 ints
-  int& bad = scratch[kSetupThreads / 64 + 1];
-  if (tid == 0) bad = 0;
+__device__ void ba_setup_phase(const BaArgs& A, const BaWs& w, char* lds, int P2) {
+  const int tid = threadIdx.x, T = blockDim.x;
+  const int E = A.E, N = A.N, t0 = A.t0;
+  int* ctl = reinterpret_cast<int*>(lds);  // [0] bad kk
+  int* scr = ctl + 64;                     // scan scratch (T/64 + 1)
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(lds + kCtlBytes);
+  int* ints = reinterpret_cast<int*>(lds + kCtlBytes);  // aliases keys once they are consumed
+  if (tid == 0) ctl[0] = 0;
   __syncthreads();
-  for (int i = tid; i < P2; i += nt) {
+  for (int i = tid; i < P2; i += T) {
     unsigned long long k = ~0ull;
     if (i < E) {
-      int64_t v = kk[i];
-      if (v < 0 || v >= num_patches) {
-        bad = 1;
-        v = v < 0 ? 0 : num_patches - 1;
+      int64_t v = A.kk[i];
+      if (v < 0 || v >= A.num_patches) {
+        ctl[0] = 1;
+        v = v < 0 ? 0 : A.num_patches - 1;
       }
       k = ((unsigned long long)v << 32) | (unsigned)i;
     }
     keys[i] = k;
   }
   __syncthreads();
-  // bitonic sort (ascending) of P2 keys
-  for (int size = 2; size <= P2; size <<= 1) {
+  for (int size = 2; size <= P2; size <<= 1) {  // bitonic sort, ascending
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < P2 / 2; i += nt) {
+      for (int i = tid; i < P2 / 2; i += T) {
         const int lo = 2 * i - (i & (stride - 1));
         const int hi = lo + stride;
         const bool up = ((lo & size) == 0);
@@ -163,91 +216,132 @@ __global__ void __launch_bounds__(kSetupThreads)
       __syncthreads();
     }
   }
-  for (int i = tid; i < E; i += nt) {
-    w.pedge[i] = (int)(keys[i] & 0xffffffffu);
-    w.skey[i] = (int64_t)(keys[i] >> 32);
-  }
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(keys);  // keys no longer needed
-  for (int i = tid; i < E; i += nt) flag[i] = (i == 0 || w.skey[i] != w.skey[i - 1]) ? 1 : 0;
-  __syncthreads();
-  // heads must be read before the scan overwrites them: keep a copy in poff
-  for (int i = tid; i < E; i += nt) w.poff[i] = flag[i];
-  __syncthreads();
-  const int nuniq = block_exclusive_scan(flag, E, scratch);
-  for (int i = tid; i < E; i += nt) {
-    const int r = flag[i] + w.poff[i] - 1;  // rank of this sorted position
-    w.ku[w.pedge[i]] = r;
-    flag[i] = r;
-  }
-  __syncthreads();
-  for (int i = tid; i < E; i += nt) {
-    if (i == 0 || flag[i] != flag[i - 1]) {
-      w.kx[flag[i]] = w.skey[i];
-      w.poff[flag[i]] = i;
+  // heads of equal-kk runs, kept in registers while the keys region is reused
+  int pe[kPerThread], kv[kPerThread], hd[kPerThread];
+#pragma unroll
+  for (int k = 0; k < kPerThread; k++) {
+    const int i = tid + k * T;
+    pe[k] = kv[k] = hd[k] = 0;
+    if (i < E) {
+      const unsigned long long v = keys[i];
+      pe[k] = (int)(v & 0xffffffffu);
+      kv[k] = (int)(v >> 32);
+      hd[k] = (i == 0 || (int)(keys[i - 1] >> 32) != kv[k]) ? 1 : 0;
     }
   }
   __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPerThread; k++) {
+    const int i = tid + k * T;
+    if (i < E) ints[i] = hd[k];
+  }
+  __syncthreads();
+  const int nuniq = block_exclusive_scan(ints, E, scr);
+#pragma unroll
+  for (int k = 0; k < kPerThread; k++) {
+    const int i = tid + k * T;
+    if (i < E) {
+      w.pedge[i] = pe[k];
+      if (hd[k]) {
+        const int r = ints[i];
+        w.kx[r] = kv[k];
+        w.poff[r] = i;
+      }
+    }
+  }
   if (tid == 0) {
     w.poff[nuniq] = E;
     w.meta[0] = nuniq;
-    w.meta[1] = bad ? 2 : 0;
-    w.meta[3] = num_patches;
+    w.meta[1] = ctl[0] ? 2 : 0;
+    w.meta[3] = A.num_patches;
   }
   __syncthreads();
-  // ---- per-patch free-pose lists (N <= 32: one bit per free pose) ----
-  int* cnt = flag;
-  for (int u = tid; u < nuniq; u += nt) {
+  // per-patch free-pose masks (N <= 20 < 32) and pose-block offsets
+  for (int u = tid; u < nuniq; u += T) {
     unsigned mask = 0;
     for (int t = w.poff[u]; t < w.poff[u + 1]; t++) {
       const int e = w.pedge[t];
-      const int64_t pi = ii[e] - t0, pj = jj[e] - t0;
-      if (pi >= 0 && pi < N) mask |= 1u << pi;
-      if (pj >= 0 && pj < N) mask |= 1u << pj;
+      const int64_t pi = A.ii[e] - t0, pj = A.jj[e] - t0;
+      if (is_free(pi, N)) mask |= 1u << pi;
+      if (is_free(pj, N)) mask |= 1u << pj;
     }
-    cnt[u] = __popc(mask);
+    w.pmask[u] = mask;
+    ints[u] = __popc(mask);
   }
   __syncthreads();
-  const int nblocks = block_exclusive_scan(cnt, nuniq, scratch);
-  for (int u = tid; u < nuniq; u += nt) w.boff[u] = cnt[u];
-  if (tid == 0) {
-    w.boff[nuniq] = nblocks;
-    w.meta[2] = nblocks;
-  }
-  __syncthreads();
-  // slot(p) = number of distinct free poses < p in the patch (ascending list)
-  for (int u = tid; u < nuniq; u += nt) {
-    unsigned mask = 0;
-    const int a = w.poff[u], b = w.poff[u + 1];
-    for (int t = a; t < b; t++) {
-      const int e = w.pedge[t];
-      const int64_t pi = ii[e] - t0, pj = jj[e] - t0;
-      if (pi >= 0 && pi < N) mask |= 1u << pi;
-      if (pj >= 0 && pj < N) mask |= 1u << pj;
-    }
-    const int base = w.boff[u];
+  const int nblocks = block_exclusive_scan(ints, nuniq, scr);
+  for (int u = tid; u < nuniq; u += T) {
+    const int base = ints[u];
+    const unsigned mask = w.pmask[u];
+    w.boff[u] = base;
     for (unsigned m = mask; m; m &= m - 1) {
       const int p = __ffs(m) - 1;
       w.bpose[base + __popc(mask & ((1u << p) - 1u))] = p;
     }
-    for (int t = a; t < b; t++) {
-      const int e = w.pedge[t];
-      const int64_t pi = ii[e] - t0, pj = jj[e] - t0;
-      w.eslot[2 * e + 0] = (pi >= 0 && pi < N) ? __popc(mask & ((1u << pi) - 1u)) : -1;
-      w.eslot[2 * e + 1] = (pj >= 0 && pj < N) ? __popc(mask & ((1u << pj) - 1u)) : -1;
+  }
+  if (tid == 0) {
+    w.boff[nuniq] = nblocks;
+    w.meta[2] = nblocks;
+  }
+  if (N == 0) {
+    if (tid == 0) w.eoff[0] = w.qoff[0] = 0;
+    __syncthreads();
+    return;
+  }
+  __syncthreads();
+  // per-pose edge lists: counts matrix [pose][thread] over contiguous edge
+  // chunks, one scan, then every thread fills its own cells (ascending edges)
+  const int ch = (E + T - 1) / T, elo = min(tid * ch, E), ehi = min(elo + ch, E);
+  for (int p = 0; p < N; p++) ints[p * T + tid] = 0;
+  for (int e = elo; e < ehi; e++) {
+    const int64_t pi = A.ii[e] - t0, pj = A.jj[e] - t0;
+    if (is_free(pi, N)) ints[pi * T + tid]++;
+    if (is_free(pj, N) && pj != pi) ints[pj * T + tid]++;
+  }
+  __syncthreads();
+  int total = block_exclusive_scan(ints, N * T, scr);
+  if (tid < N) w.eoff[tid] = ints[tid * T];
+  if (tid == 0) w.eoff[N] = total;
+  __syncthreads();
+  for (int e = elo; e < ehi; e++) {
+    const int64_t pi = A.ii[e] - t0, pj = A.jj[e] - t0;
+    const bool fi = is_free(pi, N), fj = is_free(pj, N);
+    if (fi) {
+      const int roles = 1 | ((pj == pi) ? 2 : 0);
+      const int other = (fj && pj != pi) ? (int)pj : kNoPose;
+      w.elist[ints[pi * T + tid]++] = (e << 8) | (other << 2) | roles;
+    }
+    if (fj && pj != pi) {
+      const int other = fi ? (int)pi : kNoPose;
+      w.elist[ints[pj * T + tid]++] = (e << 8) | (other << 2) | 2;
     }
   }
+  __syncthreads();
+  // per-pose patch lists, same construction over patch chunks
+  const int cu = (nuniq + T - 1) / T, ulo = min(tid * cu, nuniq), uhi = min(ulo + cu, nuniq);
+  for (int p = 0; p < N; p++) ints[p * T + tid] = 0;
+  for (int u = ulo; u < uhi; u++)
+    for (unsigned m = w.pmask[u]; m; m &= m - 1) ints[(__ffs(m) - 1) * T + tid]++;
+  __syncthreads();
+  total = block_exclusive_scan(ints, N * T, scr);
+  if (tid < N) w.qoff[tid] = ints[tid * T];
+  if (tid == 0) w.qoff[N] = total;
+  __syncthreads();
+  for (int u = ulo; u < uhi; u++)
+    for (unsigned m = w.pmask[u]; m; m &= m - 1) w.qlist[ints[(__ffs(m) - 1) * T + tid]++] = u;
+  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
-// linearize: one thread per unique patch.  fp32 edge math exactly as
-// reprojection_residuals_and_hessian (ba_cuda.cu:265-333); patch sums in fp64.
+// LINEARIZE: fp32 edge math exactly as reprojection_residuals_and_hessian
+// (ba_cuda.cu:265-333), contraction off so it rounds like the reference's
+// source order; then the edge's E blocks, C and u terms in fp64.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void edge_linearize(const float* __restrict__ poses,
-                                               const float* __restrict__ patches, int P, float fx,
-                                               float fy, float cx, float cy, float tx, float ty,
-                                               float wx, float wy, int ix, int jx, int64_t kx,
-                                               float* __restrict__ o) {
+#pragma clang fp contract(off)
+__device__ __forceinline__ void edge_linearize(const float* poses, const float* patches, int P,
+                                               float fx, float fy, float cx, float cy, float tx,
+                                               float ty, float wx, float wy, int ix, int jx,
+                                               int64_t kx, float* o) {
   const float* pi = poses + 7 * (size_t)ix;
   const float* pj = poses + 7 * (size_t)jx;
   const float* pk = patches + (size_t)kx * 3 * P * P;
@@ -263,7 +357,7 @@ __device__ __forceinline__ void edge_linearize(const float* __restrict__ poses,
   relSE3(ti, qi, tj, qj, tij, qij);
   actSE3(tij, qij, Xi, Xj);
   const float X = Xj[0], Y = Xj[1], Z = Xj[2], W = Xj[3];
-  const float d = ((double)Z >= 0.2) ? 1.0f / Z : 0.0f;  // ba_cuda.cu:296
+  const float d = ((double)Z >= 0.2) ? (float)(1.0 / (double)Z) : 0.0f;  // ba_cuda.cu:296
   const float d2 = d * d;
   const float x1 = fx * (X / Z) + cx;
   const float y1 = fy * (Y / Z) + cy;
@@ -294,279 +388,7 @@ __device__ __forceinline__ void edge_linearize(const float* __restrict__ poses,
   }
 }
 
-__global__ void __launch_bounds__(256)
-    ba_linearize_kernel(const float* __restrict__ poses, const float* __restrict__ patches,
-                        const float* __restrict__ intrinsics, const float* __restrict__ target,
-                        const float* __restrict__ weight, const float* __restrict__ lmbda,
-                        const int64_t* __restrict__ ii, const int64_t* __restrict__ jj,
-                        const int64_t* __restrict__ kk, int P, int num_poses, BaWs w) {
-  const int u = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nuniq = w.meta[0];
-  if (u >= nuniq) return;
-  const float fx = intrinsics[0], fy = intrinsics[1], cx = intrinsics[2], cy = intrinsics[3];
-  const double lam = (double)lmbda[0];
-  const int a = w.poff[u], b = w.poff[u + 1];
-  const int b0 = w.boff[u], nb = w.boff[u + 1] - b0;
-  double* cbp = w.cb + 6 * (size_t)b0;
-  for (int i = 0; i < 6 * nb; i++) cbp[i] = 0.0;
-  double C = 0.0, Uu = 0.0;
-  for (int t = a; t < b; t++) {
-    const int e = w.pedge[t];
-    int ix = (int)ii[e], jx = (int)jj[e];
-    ix = min(max(ix, 0), num_poses - 1);  // memory guard (reference: unchecked)
-    jx = min(max(jx, 0), num_poses - 1);
-    float* o = w.J + (size_t)kJStride * e;
-    const int64_t kx = min(max(kk[e], (int64_t)0), (int64_t)w.meta[3] - 1);
-    edge_linearize(poses, patches, P, fx, fy, cx, cy, target[2 * e], target[2 * e + 1],
-                   weight[2 * e], weight[2 * e + 1], ix, jx, kx, o);
-    const int si = w.eslot[2 * e], sj = w.eslot[2 * e + 1];
-    for (int row = 0; row < 2; row++) {
-      const double wr = o[row];
-      const float r = o[2 + row], Jz = o[4 + row];
-      const float* Ji = o + 6 + 6 * row;
-      const float* Jj = o + 18 + 6 * row;
-      for (int k = 0; k < 6; k++) {  // E blocks (ba_cuda.cu:352-363)
-        if (si >= 0) cbp[6 * si + k] -= wr * Jz * Ji[k];
-        if (sj >= 0) cbp[6 * sj + k] += wr * Jz * Jj[k];
-      }
-      C += wr * Jz * Jz;  // :372-373
-      Uu += wr * r * Jz;
-    }
-  }
-  w.Q[u] = 1.0 / (C + lam);  // :519
-  w.U[u] = Uu;
-}
-
-// ---------------------------------------------------------------------------
-// schur: one workgroup per lower 6x6 block (a, b), a >= b, of
-//   S = B - E Q E^T  and (diagonal blocks) y = v - E Q u.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void tri_decode(int t, int* a, int* b) {
-  int r = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-  while (r * (r + 1) / 2 > t) r--;
-  while ((r + 1) * (r + 2) / 2 <= t) r++;
-  *a = r;
-  *b = t - r * (r + 1) / 2;
-}
-
-__global__ void __launch_bounds__(kSchurThreads)
-    ba_schur_kernel(const int64_t* __restrict__ ii, const int64_t* __restrict__ jj, int E, int t0,
-                    int N, BaWs w, double* __restrict__ S_out, double* __restrict__ y_out) {
-  __shared__ double red[42][kSchurThreads / 64];
-  int pa, pb;
-  tri_decode(blockIdx.x, &pa, &pb);
-  const bool diag = pa == pb;
-  const int tid = threadIdx.x;
-  double acc[36], yacc[6];
-#pragma unroll
-  for (int i = 0; i < 36; i++) acc[i] = 0.0;
-#pragma unroll
-  for (int i = 0; i < 6; i++) yacc[i] = 0.0;
-
-  // ---- B and v terms (ba_cuda.cu:339-370) ----
-  for (int e = tid; e < E; e += kSchurThreads) {
-    const int64_t pi = ii[e] - t0, pj = jj[e] - t0;
-    const bool fi = pi >= 0 && pi < N, fj = pj >= 0 && pj < N;
-    int mode = 0;  // bit0: +JiJi^T, bit1: +JjJj^T, bit2: -(JiJj^T+JjJi^T), bit3: -JiJj^T, bit4: -JjJi^T
-    if (diag) {
-      if (fi && pi == pa) mode |= 1;
-      if (fj && pj == pa) mode |= 2;
-      if (fi && fj && pi == pa && pj == pa) mode |= 4;
-    } else {
-      if (fi && fj && pi == pa && pj == pb) mode |= 8;
-      if (fi && fj && pj == pa && pi == pb) mode |= 16;
-    }
-    if (!mode) continue;
-    const float* o = w.J + (size_t)kJStride * e;
-    for (int row = 0; row < 2; row++) {
-      const double wr = o[row];
-      const float r = o[2 + row];
-      const float* Ji = o + 6 + 6 * row;
-      const float* Jj = o + 18 + 6 * row;
-      float ji[6], jv[6];
-#pragma unroll
-      for (int k = 0; k < 6; k++) { ji[k] = Ji[k]; jv[k] = Jj[k]; }
-#pragma unroll
-      for (int x = 0; x < 6; x++)
-#pragma unroll
-        for (int z = 0; z < 6; z++) {
-          double s = 0.0;
-          if (mode & 1) s += wr * ji[x] * ji[z];
-          if (mode & 2) s += wr * jv[x] * jv[z];
-          if (mode & 4) s -= wr * ji[x] * jv[z] + wr * jv[x] * ji[z];
-          if (mode & 8) s -= wr * ji[x] * jv[z];
-          if (mode & 16) s -= wr * jv[x] * ji[z];
-          acc[x * 6 + z] += s;
-        }
-      if (diag) {
-#pragma unroll
-        for (int x = 0; x < 6; x++) {
-          if (mode & 1) yacc[x] -= wr * r * ji[x];
-          if (mode & 2) yacc[x] += wr * r * jv[x];
-        }
-      }
-    }
-  }
-  // ---- E Q E^T and E Q u terms (ba_cuda.cu:554-558) ----
-  const int nuniq = w.meta[0];
-  for (int u = tid; u < nuniq; u += kSchurThreads) {
-    const int b0 = w.boff[u], b1 = w.boff[u + 1];
-    int sa = -1, sb = -1;
-    for (int s = b0; s < b1; s++) {
-      const int p = w.bpose[s];
-      if (p == pa) sa = s;
-      if (p == pb) sb = s;
-    }
-    if (sa < 0 || sb < 0) continue;
-    const double q = w.Q[u];
-    const double* ca = w.cb + 6 * (size_t)sa;
-    const double* cbb = w.cb + 6 * (size_t)sb;
-    double va[6], vb[6];
-#pragma unroll
-    for (int k = 0; k < 6; k++) { va[k] = ca[k]; vb[k] = cbb[k]; }
-#pragma unroll
-    for (int x = 0; x < 6; x++)
-#pragma unroll
-      for (int z = 0; z < 6; z++) acc[x * 6 + z] -= va[x] * q * vb[z];
-    if (diag) {
-      const double qu = q * w.U[u];
-#pragma unroll
-      for (int x = 0; x < 6; x++) yacc[x] -= va[x] * qu;
-    }
-  }
-  // ---- fixed-order reduction: wave shuffles, then across waves ----
-  const int lane = tid & 63, wid = tid >> 6;
-#pragma unroll
-  for (int i = 0; i < 42; i++) {
-    double v = i < 36 ? acc[i] : yacc[i - 36];
-    v = wave_sum(v);
-    if (lane == 0) red[i][wid] = v;
-  }
-  __syncthreads();
-  if (tid < 42) {
-    double s = 0.0;
-    for (int k = 0; k < kSchurThreads / 64; k++) s += red[tid][k];
-    if (tid < 36)
-      S_out[(size_t)blockIdx.x * 36 + tid] = s;
-    else if (diag)
-      y_out[6 * pa + (tid - 36)] = s;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// solve + update (single workgroup).
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kSolveThreads)
-    ba_solve_kernel(float* __restrict__ poses, float* __restrict__ patches, int P, int num_poses,
-                    int t0, int N, const double* __restrict__ S_in, const double* __restrict__ y_in,
-                    BaWs w, double* __restrict__ dX_out) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int n = 6 * N;
-  const int ld = n + 1;  // padded row stride (banks)
-  double* S = sm;                        // [n][ld]
-  double* diagL = S + (size_t)n * ld;    // [n]
-  double* x = diagL + n;                 // [n]
-  int& fail = *reinterpret_cast<int*>(x + n);
-  const int tid = threadIdx.x, nt = blockDim.x;
-  if (tid == 0) fail = 0;
-  if (n > 0) {
-    // lower blocks -> dense lower triangle; damping S += I * (1e-4 S + 1) (ba_cuda.cu:560)
-    const int NL = N * (N + 1) / 2;
-    for (int t = tid; t < NL * 36; t += nt) {
-      const int blk = t / 36, e = t % 36;
-      int a, b;
-      tri_decode(blk, &a, &b);
-      const int r = 6 * a + e / 6, c = 6 * b + e % 6;
-      double v = S_in[t];
-      if (r == c) v += 1e-4 * v + 1.0;
-      if (c <= r) S[r * ld + c] = v;
-    }
-    for (int i = tid; i < n; i += nt) x[i] = y_in[i];
-    __syncthreads();
-    // Cholesky, right-looking; L(r,j) stored at S[j][r] (upper triangle)
-    for (int j = 0; j < n; j++) {
-      const double d = S[j * ld + j];
-      if (!(d > 0.0)) {  // uniform: every thread reads the same value
-        if (tid == 0) fail = 1;
-        break;
-      }
-      const double sd = sqrt(d), inv_d = 1.0 / d;
-      const int m = n - j - 1;
-      for (int t = tid; t < m * m; t += nt) {
-        const int r = j + 1 + t / m, c = j + 1 + t % m;
-        if (c <= r) S[r * ld + c] -= S[r * ld + j] * S[c * ld + j] * inv_d;
-      }
-      for (int r = j + 1 + tid; r < n; r += nt) S[j * ld + r] = S[r * ld + j] / sd;
-      if (tid == 0) diagL[j] = sd;
-      __syncthreads();
-    }
-    __syncthreads();
-    if (fail) {
-      for (int i = tid; i < n; i += nt) x[i] = 0.0;  // dX = 0 (dpvo/ba.py:17-21)
-    } else if (tid < 64) {
-      // forward L z = y, backward L^T x = z, one wave (wave-synchronous LDS)
-      for (int j = 0; j < n; j++) {
-        const double z = x[j] / diagL[j];
-        wave_lds_sync();
-        for (int r = j + 1 + tid; r < n; r += 64) x[r] -= S[j * ld + r] * z;
-        if (tid == 0) x[j] = z;
-        wave_lds_sync();
-      }
-      for (int j = n - 1; j >= 0; j--) {
-        const double v = x[j] / diagL[j];
-        wave_lds_sync();
-        for (int r = tid; r < j; r += 64) x[r] -= S[r * ld + j] * v;
-        if (tid == 0) x[j] = v;
-        wave_lds_sync();
-      }
-    }
-    __syncthreads();
-    for (int i = tid; i < n; i += nt) {
-      w.dX[i] = x[i];
-      if (dX_out) dX_out[i] = x[i];
-    }
-    // pose retraction poses[t0+i] <- Exp(dX_i) poses[t0+i] (pose_retr_kernel :178-206)
-    for (int i = tid; i < N; i += nt) {
-      const int t = t0 + i;
-      if (t < 0 || t >= num_poses) continue;
-      float* pt = poses + 7 * (size_t)t;
-      float xi[6], t1[3], q1[4];
-      for (int k = 0; k < 6; k++) xi[k] = (float)x[6 * i + k];
-      float tt[3] = {pt[0], pt[1], pt[2]}, qq[4] = {pt[3], pt[4], pt[5], pt[6]};
-      retrSE3(xi, tt, qq, t1, q1);
-      pt[0] = t1[0]; pt[1] = t1[1]; pt[2] = t1[2];
-      pt[3] = q1[0]; pt[4] = q1[1]; pt[5] = q1[2]; pt[6] = q1[3];
-    }
-  }
-  if (tid == 0) w.meta[1] = (w.meta[1] & ~1) | (fail ? 1 : 0);
-  // dZ = Q (u - E^T dX) and patch retraction (patch_retr_kernel :209-229)
-  const int nuniq = w.meta[0];
-  for (int u = tid; u < nuniq; u += nt) {
-    double s = w.U[u];
-    if (n > 0) {
-      for (int b = w.boff[u]; b < w.boff[u + 1]; b++) {
-        const int p = w.bpose[b];
-        const double* c = w.cb + 6 * (size_t)b;
-        for (int k = 0; k < 6; k++) s -= c[k] * x[6 * p + k];
-      }
-    }
-    const float dz = (float)(w.Q[u] * s);
-    float* pk = patches + (size_t)w.kx[u] * 3 * P * P + 2 * P * P;
-    float d = pk[0] + dz;
-    d = (d > 20.0f) ? 1.0f : d;
-    d = (float)fmax((double)d, 1e-4);
-    for (int k = 0; k < P * P; k++) pk[k] = d;
-  }
-}
-
-static size_t solve_smem(int N) {
-  const int n = 6 * N;
-  return sizeof(double) * ((size_t)n * (n + 1) + 2 * (size_t)n + 2);  // + fail flag
-}
-
-// ---------------------------------------------------------------------------
 // F-REPROJ (ba_cuda.cu:379-429): one thread per (edge, patch pixel).
-// ---------------------------------------------------------------------------
 __global__ void reproject_kernel(const float* __restrict__ poses, const float* __restrict__ patches,
                                  const float* __restrict__ intrinsics,
                                  const int64_t* __restrict__ ii, const int64_t* __restrict__ jj,
@@ -595,6 +417,571 @@ __global__ void reproject_kernel(const float* __restrict__ poses, const float* _
   actSE3(tij, qij, Xi, Xj);
   coords[((size_t)n * 2 + 0) * PP + pix] = fx * (Xj[0] / Xj[2]) + cx;
   coords[((size_t)n * 2 + 1) * PP + pix] = fy * (Xj[1] / Xj[2]) + cy;
+}
+#pragma clang fp contract(fast)
+
+__device__ void ba_linearize_phase(const BaArgs& A, const BaWs& w) {
+  const float fx = A.intrinsics[0], fy = A.intrinsics[1], cx = A.intrinsics[2],
+              cy = A.intrinsics[3];
+  const int64_t kmax = (int64_t)w.meta[3] - 1;  // patch count recorded by the setup
+  for (int e = threadIdx.x; e < A.E; e += blockDim.x) {
+    const int ix = (int)min(max(A.ii[e], (int64_t)0), (int64_t)A.num_poses - 1);
+    const int jx = (int)min(max(A.jj[e], (int64_t)0), (int64_t)A.num_poses - 1);
+    const int64_t kx = min(max(A.kk[e], (int64_t)0), kmax);  // memory guard (reference: unchecked)
+    float o[30];
+    edge_linearize(A.poses, A.patches, A.P, fx, fy, cx, cy, A.target[2 * e], A.target[2 * e + 1],
+                   A.weight[2 * e], A.weight[2 * e + 1], ix, jx, kx, o);
+    float4* Jo = reinterpret_cast<float4*>(w.J + (size_t)kJStride * e);
+#pragma unroll
+    for (int k = 0; k < 7; k++) Jo[k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+    reinterpret_cast<float2*>(Jo + 7)[0] = make_float2(o[28], o[29]);
+    double ec[14];
+#pragma unroll
+    for (int k = 0; k < 14; k++) ec[k] = 0.0;
+#pragma unroll
+    for (int row = 0; row < 2; row++) {  // ba_cuda.cu:352-373
+      const double wr = o[row];
+      const float r = o[2 + row], Jz = o[4 + row];
+      const double wz = wr * Jz;
+#pragma unroll
+      for (int k = 0; k < 6; k++) {
+        ec[k] -= wz * o[6 + 6 * row + k];
+        ec[6 + k] += wz * o[18 + 6 * row + k];
+      }
+      ec[12] += wz * Jz;
+      ec[13] += wr * r * Jz;
+    }
+    double2* Eo = reinterpret_cast<double2*>(w.EC + (size_t)kEStride * e);
+#pragma unroll
+    for (int k = 0; k < 7; k++) Eo[k] = make_double2(ec[2 * k], ec[2 * k + 1]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// PATCH: Q_u = 1/(C_u + lmbda), U_u, and c_{u,p} = sum of the E blocks of
+// pose p over the patch's edges (ascending edge order).
+// ---------------------------------------------------------------------------
+__device__ void ba_patch_phase(const BaArgs& A, const BaWs& w) {
+  const double lam = (double)A.lmbda[0];
+  const int nuniq = w.meta[0];
+  for (int u = threadIdx.x; u < nuniq; u += blockDim.x) {
+    const int a = w.poff[u], b = w.poff[u + 1];
+    double C = 0.0, Uu = 0.0;
+    for (int t = a; t < b; t++) {
+      const double* ec = w.EC + (size_t)kEStride * w.pedge[t];
+      C += ec[12];
+      Uu += ec[13];
+    }
+    w.Q[u] = 1.0 / (C + lam);  // ba_cuda.cu:519
+    w.U[u] = Uu;
+    for (int s = w.boff[u]; s < w.boff[u + 1]; s++) {
+      const int p = w.bpose[s];
+      double c[6] = {0, 0, 0, 0, 0, 0};
+      for (int t = a; t < b; t++) {
+        const int e = w.pedge[t];
+        const double* ec = w.EC + (size_t)kEStride * e;
+        const int64_t pi = A.ii[e] - A.t0, pj = A.jj[e] - A.t0;
+        if (pi == p)
+#pragma unroll
+          for (int k = 0; k < 6; k++) c[k] += ec[k];
+        if (pj == p)
+#pragma unroll
+          for (int k = 0; k < 6; k++) c[k] += ec[6 + k];
+      }
+      double2* co = reinterpret_cast<double2*>(w.cb + 6 * (size_t)s);
+      co[0] = make_double2(c[0], c[1]);
+      co[1] = make_double2(c[2], c[3]);
+      co[2] = make_double2(c[4], c[5]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// SCHUR: S = B - E Q E^T (lower 6x6 blocks), y = v - E Q u.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_row(const float* o, int row, double& wr, float& r, float* ji,
+                                         float* jv) {
+  wr = o[row];
+  r = o[2 + row];
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    ji[k] = o[6 + 6 * row + k];
+    jv[k] = o[18 + 6 * row + k];
+  }
+}
+
+template <int NV>
+__device__ __forceinline__ void team_reduce(double* v, int tau) {
+  for (int o = tau >> 1; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < NV; i++) v[i] += __shfl_xor(v[i], o, 64);
+}
+
+// diagonal block (a, a) and y_a; team of tau lanes (tau | 64)
+__device__ void schur_diag(const BaWs& w, int a, int lane, int tau, double* Sout, double* yout) {
+  double acc[21], yv[6];
+#pragma unroll
+  for (int i = 0; i < 21; i++) acc[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; i++) yv[i] = 0.0;
+  const int e1 = w.eoff[a + 1];
+  for (int t = w.eoff[a] + lane; t < e1; t += tau) {  // B_aa, v_a (ba_cuda.cu:339-370)
+    const int ent = w.elist[t];
+    const int roles = ent & 3;
+    const float* o = w.J + (size_t)kJStride * (ent >> 8);
+#pragma unroll
+    for (int row = 0; row < 2; row++) {
+      double wr;
+      float r, ji[6], jv[6];
+      load_row(o, row, wr, r, ji, jv);
+      const double wrr = wr * r;
+      if (roles & 1) {
+#pragma unroll
+        for (int x = 0, q = 0; x < 6; x++) {
+          const double wx = wr * ji[x];
+#pragma unroll
+          for (int z = 0; z <= x; z++, q++) acc[q] += wx * ji[z];
+          yv[x] -= wrr * ji[x];
+        }
+      }
+      if (roles & 2) {
+#pragma unroll
+        for (int x = 0, q = 0; x < 6; x++) {
+          const double wx = wr * jv[x];
+#pragma unroll
+          for (int z = 0; z <= x; z++, q++) acc[q] += wx * jv[z];
+          yv[x] += wrr * jv[x];
+        }
+      }
+      if (roles == 3) {  // ii == jj: both cross terms land on the diagonal block
+#pragma unroll
+        for (int x = 0, q = 0; x < 6; x++)
+#pragma unroll
+          for (int z = 0; z <= x; z++, q++) acc[q] -= wr * ji[x] * jv[z] + wr * jv[x] * ji[z];
+      }
+    }
+  }
+  const int q1 = w.qoff[a + 1];
+  for (int t = w.qoff[a] + lane; t < q1; t += tau) {  // E Q E^T, E Q u (:554-558)
+    const int u = w.qlist[t];
+    const unsigned mask = w.pmask[u];
+    const int s = w.boff[u] + __popc(mask & ((1u << a) - 1u));
+    const double2* cp = reinterpret_cast<const double2*>(w.cb + 6 * (size_t)s);
+    const double2 c01 = cp[0], c23 = cp[1], c45 = cp[2];
+    const double c[6] = {c01.x, c01.y, c23.x, c23.y, c45.x, c45.y};
+    const double q = w.Q[u], qu = q * w.U[u];
+#pragma unroll
+    for (int x = 0, k = 0; x < 6; x++) {
+      const double cq = c[x] * q;
+#pragma unroll
+      for (int z = 0; z <= x; z++, k++) acc[k] -= cq * c[z];
+      yv[x] -= c[x] * qu;
+    }
+  }
+  team_reduce<21>(acc, tau);
+  team_reduce<6>(yv, tau);
+  double* Sb = Sout + 36 * (size_t)blk(a, a);
+#pragma unroll
+  for (int x = 0, k = 0; x < 6; x++)
+#pragma unroll
+    for (int z = 0; z <= x; z++, k++)
+      if ((k % tau) == lane) {
+        Sb[6 * x + z] = acc[k];
+        Sb[6 * z + x] = acc[k];
+      }
+#pragma unroll
+  for (int x = 0; x < 6; x++)
+    if (((21 + x) % tau) == lane) yout[6 * a + x] = yv[x];
+}
+
+// off-diagonal block (a, b), a > b: walks the shorter of the two pose lists
+__device__ void schur_off(const BaWs& w, int a, int b, int lane, int tau, double* Sout) {
+  double acc[36];
+#pragma unroll
+  for (int i = 0; i < 36; i++) acc[i] = 0.0;
+  const int la = w.eoff[a + 1] - w.eoff[a], lb = w.eoff[b + 1] - w.eoff[b];
+  const int sp = (lb < la) ? b : a, other = (sp == a) ? b : a;
+  const int e1 = w.eoff[sp + 1];
+  for (int t = w.eoff[sp] + lane; t < e1; t += tau) {  // B_ab = -sum w Ji_a^T Jj_b
+    const int ent = w.elist[t];
+    if (((ent >> 2) & 31) != other) continue;
+    // rows of the block follow pose a: Ji when ii == a, Jj when jj == a
+    const bool rows_i = (sp == a) ? (ent & 1) : (ent & 2);
+    const float* o = w.J + (size_t)kJStride * (ent >> 8);
+    const float* orow = o + (rows_i ? 6 : 18);
+    const float* ocol = o + (rows_i ? 18 : 6);
+#pragma unroll 1
+    for (int row = 0; row < 2; row++) {
+      const double wr = o[row];
+      float rx[6], cz[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) {
+        rx[k] = orow[6 * row + k];
+        cz[k] = ocol[6 * row + k];
+      }
+#pragma unroll
+      for (int x = 0; x < 6; x++) {
+        const double wx = wr * rx[x];
+#pragma unroll
+        for (int z = 0; z < 6; z++) acc[6 * x + z] -= wx * cz[z];
+      }
+    }
+  }
+  const int qa = w.qoff[a + 1] - w.qoff[a], qb = w.qoff[b + 1] - w.qoff[b];
+  const int qp = (qb < qa) ? b : a, qo = (qp == a) ? b : a;
+  const int q1 = w.qoff[qp + 1];
+  for (int t = w.qoff[qp] + lane; t < q1; t += tau) {
+    const int u = w.qlist[t];
+    const unsigned mask = w.pmask[u];
+    if (!((mask >> qo) & 1u)) continue;
+    const int s0 = w.boff[u];
+    const double* ca = w.cb + 6 * (size_t)(s0 + __popc(mask & ((1u << a) - 1u)));
+    const double* cc = w.cb + 6 * (size_t)(s0 + __popc(mask & ((1u << b) - 1u)));
+    double va[6], vb[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      va[k] = ca[k];
+      vb[k] = cc[k];
+    }
+    const double q = w.Q[u];
+#pragma unroll
+    for (int x = 0; x < 6; x++) {
+      const double cq = va[x] * q;
+#pragma unroll
+      for (int z = 0; z < 6; z++) acc[6 * x + z] -= cq * vb[z];
+    }
+  }
+  team_reduce<36>(acc, tau);
+  double* Sb = Sout + 36 * (size_t)blk(a, b);
+#pragma unroll
+  for (int k = 0; k < 36; k++)
+    if ((k % tau) == lane) Sb[k] = acc[k];
+}
+
+__device__ __forceinline__ int pow2_floor(int v) {
+  int p = 1;
+  while (2 * p <= v) p *= 2;
+  return p;
+}
+
+__device__ void ba_schur_phase(const BaWs& w, int N, double* Sout, double* yout) {
+  const int tid = threadIdx.x, T = blockDim.x;
+  // diagonal blocks (the heavy ones): one team of up to a wave each
+  {
+    const int tau = min(64, pow2_floor(T / N));
+    const int team = tid / tau, lane = tid % tau, nteam = T / tau;
+    for (int a = team; a < N; a += nteam) schur_diag(w, a, lane, tau, Sout, yout);
+  }
+  // off-diagonal blocks, assigned from the last team down so they land on
+  // the waves the diagonal pass left idle
+  const int noff = N * (N - 1) / 2;
+  if (noff > 0) {
+    const int tau = min(64, pow2_floor(max(1, T / noff)));
+    const int nteam = T / tau, team = nteam - 1 - tid / tau, lane = tid % tau;
+    for (int d = team; d < noff; d += nteam) {
+      const int a = 1 + tri_row(d), b = d - a * (a - 1) / 2;  // a > b
+      schur_off(w, a, b, lane, tau, Sout);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// SOLVE: S (lower blocks, LDS) -> L; y -> x.  L_kk^{-1} kept per block.
+// ---------------------------------------------------------------------------
+// one lane: in-place Cholesky of the 6x6 block (lower), its inverse to Li.
+// Packed lower storage (21 doubles each) keeps it in registers.
+__device__ __forceinline__ constexpr int lt(int r, int c) { return r * (r + 1) / 2 + c; }
+
+__device__ __noinline__ void factor_diag(double* Sb, double* Li, int* fail) {
+  double L[21], inv[6];
+#pragma unroll
+  for (int r = 0; r < 6; r++)
+#pragma unroll
+    for (int c = 0; c <= r; c++) L[lt(r, c)] = Sb[6 * r + c];
+  bool ok = true;
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+    const double d = L[lt(c, c)];
+    ok = ok && (d > 0.0);
+    const double s = sqrt(d);
+    inv[c] = 1.0 / s;
+    L[lt(c, c)] = s;
+#pragma unroll
+    for (int r = c + 1; r < 6; r++) L[lt(r, c)] *= inv[c];
+#pragma unroll
+    for (int c2 = c + 1; c2 < 6; c2++)
+#pragma unroll
+      for (int r = c2; r < 6; r++) L[lt(r, c2)] -= L[lt(r, c)] * L[lt(c2, c)];
+  }
+#pragma unroll
+  for (int r = 0; r < 6; r++)
+#pragma unroll
+    for (int c = 0; c < 6; c++) Sb[6 * r + c] = c <= r ? L[lt(r, c)] : 0.0;
+  double X[21];  // X = L^{-1}, lower
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    X[lt(i, i)] = inv[i];
+#pragma unroll
+    for (int j = 0; j < i; j++) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = j; k < i; k++) s += L[lt(i, k)] * X[lt(k, j)];
+      X[lt(i, j)] = -s * inv[i];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 6; r++)
+#pragma unroll
+    for (int c = 0; c < 6; c++) Li[6 * r + c] = (ok && c <= r) ? X[lt(r, c)] : 0.0;
+  if (!ok) *fail = 1;
+}
+
+// x = dX in y (LDS); returns through LDS.  All threads call.
+__device__ void ba_solve_phase(int N, double* S, double* Linv, double* y, int* fail) {
+  const int tid = threadIdx.x, T = blockDim.x;
+  if (tid == 0) *fail = 0;
+  for (int t = tid; t < 6 * N; t += T) {  // S += I * (1e-4 S + 1)  (ba_cuda.cu:560)
+    double* d = S + 36 * (size_t)blk(t / 6, t / 6) + 7 * (t % 6);
+    *d += 1e-4 * *d + 1.0;
+  }
+  __syncthreads();
+  if (tid == 0) factor_diag(S, Linv, fail);
+  __syncthreads();
+  for (int k = 0; k < N; k++) {
+    const int m = N - k - 1;  // remaining poses below k
+    const double* Lk = Linv + 36 * k;
+    // panel: L_ak = S_ak L_kk^{-T}
+    for (int t = tid; t < 6 * m; t += T) {
+      const int a = k + 1 + t / 6, r = t % 6;
+      double* row = S + 36 * (size_t)blk(a, k) + 6 * r;
+      double s[6], o[6];
+#pragma unroll
+      for (int c = 0; c < 6; c++) s[c] = row[c];
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q <= c; q++) v += s[q] * Lk[6 * c + q];
+        o[c] = v;
+      }
+#pragma unroll
+      for (int c = 0; c < 6; c++) row[c] = o[c];
+    }
+    __syncthreads();
+    if (m == 0) break;
+    // trailing: S_ab -= L_ak L_bk^T for k < b <= a; wave 0 updates block
+    // (k+1, k+1) and factors it while the other waves do the rest
+    if (tid < 64) {
+      if (tid < 6) {
+        const double* la = S + 36 * (size_t)blk(k + 1, k) + 6 * tid;
+        double* row = S + 36 * (size_t)blk(k + 1, k + 1) + 6 * tid;
+        double lr[6];
+#pragma unroll
+        for (int q = 0; q < 6; q++) lr[q] = la[q];
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+          const double* lc = S + 36 * (size_t)blk(k + 1, k) + 6 * c;
+          double v = row[c];
+#pragma unroll
+          for (int q = 0; q < 6; q++) v -= lr[q] * lc[q];
+          row[c] = v;
+        }
+      }
+      wave_lds_sync();
+      if (tid == 0) factor_diag(S + 36 * (size_t)blk(k + 1, k + 1), Linv + 36 * (k + 1), fail);
+    } else {
+      const int ntask = 6 * (m * (m + 1) / 2 - 1);
+      for (int t = tid - 64; t < ntask; t += T - 64) {
+        const int j = 1 + t / 6, r = t % 6;
+        const int ap = tri_row(j), bp = j - ap * (ap + 1) / 2;
+        const int a = k + 1 + ap, b = k + 1 + bp;
+        const double* la = S + 36 * (size_t)blk(a, k) + 6 * r;
+        double* row = S + 36 * (size_t)blk(a, b) + 6 * r;
+        double lr[6];
+#pragma unroll
+        for (int q = 0; q < 6; q++) lr[q] = la[q];
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+          const double* lc = S + 36 * (size_t)blk(b, k) + 6 * c;
+          double v = row[c];
+#pragma unroll
+          for (int q = 0; q < 6; q++) v -= lr[q] * lc[q];
+          row[c] = v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (*fail) {
+    for (int t = tid; t < 6 * N; t += T) y[t] = 0.0;  // dX = 0 (dpvo/ba.py:17-21)
+  } else if (tid < 64) {
+    // forward: z_k = L_kk^{-1} (y_k - sum_{b<k} L_kb z_b), right-looking
+    for (int k = 0; k < N; k++) {
+      double z = 0.0;
+      if (tid < 6) {
+        const double* Lk = Linv + 36 * k + 6 * tid;
+#pragma unroll
+        for (int c = 0; c < 6; c++) z += Lk[c] * y[6 * k + c];
+      }
+      wave_lds_sync();
+      if (tid < 6) y[6 * k + tid] = z;
+      wave_lds_sync();
+      for (int t = tid; t < 6 * (N - k - 1); t += 64) {
+        const int a = k + 1 + t / 6, r = t % 6;
+        const double* la = S + 36 * (size_t)blk(a, k) + 6 * r;
+        double v = y[6 * a + r];
+#pragma unroll
+        for (int c = 0; c < 6; c++) v -= la[c] * y[6 * k + c];
+        y[6 * a + r] = v;
+      }
+      wave_lds_sync();
+    }
+    // backward: x_k = L_kk^{-T} (z_k - sum_{a>k} L_ak^T x_a)
+    for (int k = N - 1; k >= 0; k--) {
+      double x = 0.0;
+      if (tid < 6) {
+#pragma unroll
+        for (int c = 0; c < 6; c++) x += Linv[36 * k + 6 * c + tid] * y[6 * k + c];
+      }
+      wave_lds_sync();
+      if (tid < 6) y[6 * k + tid] = x;
+      wave_lds_sync();
+      for (int t = tid; t < 6 * k; t += 64) {
+        const int b = t / 6, r = t % 6;
+        const double* lk = S + 36 * (size_t)blk(k, b);
+        double v = y[6 * b + r];
+#pragma unroll
+        for (int c = 0; c < 6; c++) v -= lk[6 * c + r] * y[6 * k + c];
+        y[6 * b + r] = v;
+      }
+      wave_lds_sync();
+    }
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// UPDATE: pose_retr_kernel (:178-206), dZ (:563), patch_retr_kernel (:209-229)
+// ---------------------------------------------------------------------------
+__device__ void ba_update_phase(const BaArgs& A, const BaWs& w, const double* x, int fail,
+                                double* dX_out) {
+  const int tid = threadIdx.x, T = blockDim.x, N = A.N;
+  for (int i = tid; i < 6 * N; i += T) {
+    w.dX[i] = x[i];
+    if (dX_out) dX_out[i] = x[i];
+  }
+  if (tid == 0) w.meta[1] = (w.meta[1] & ~1) | (fail ? 1 : 0);
+  for (int i = tid; i < N; i += T) {
+    const int t = A.t0 + i;
+    if (t < 0 || t >= A.num_poses) continue;
+    float* pt = A.poses + 7 * (size_t)t;
+    float xi[6], t1[3], q1[4];
+#pragma unroll
+    for (int k = 0; k < 6; k++) xi[k] = (float)x[6 * i + k];
+    float tt[3] = {pt[0], pt[1], pt[2]}, qq[4] = {pt[3], pt[4], pt[5], pt[6]};
+    retrSE3(xi, tt, qq, t1, q1);
+    pt[0] = t1[0]; pt[1] = t1[1]; pt[2] = t1[2];
+    pt[3] = q1[0]; pt[4] = q1[1]; pt[5] = q1[2]; pt[6] = q1[3];
+  }
+  const int nuniq = w.meta[0], P = A.P;
+  for (int u = tid; u < nuniq; u += T) {
+    double s = w.U[u];
+    for (int b = w.boff[u]; b < w.boff[u + 1]; b++) {
+      const int p = w.bpose[b];
+      const double* c = w.cb + 6 * (size_t)b;
+#pragma unroll
+      for (int k = 0; k < 6; k++) s -= c[k] * x[6 * p + k];
+    }
+    const float dz = (float)(w.Q[u] * s);
+    float* pk = A.patches + (size_t)w.kx[u] * 3 * P * P + 2 * P * P;
+    float d = pk[0] + dz;
+    d = (d > 20.0f) ? 1.0f : d;
+    d = (float)fmax((double)d, 1e-4);
+    for (int k = 0; k < P * P; k++) pk[k] = d;
+  }
+}
+
+// LDS carve of the solve region
+struct SolveLds {
+  int* ctl;
+  double* S;
+  double* Linv;
+  double* y;
+};
+__device__ __forceinline__ SolveLds solve_carve(char* lds, int N) {
+  SolveLds s;
+  s.ctl = reinterpret_cast<int*>(lds);
+  s.S = reinterpret_cast<double*>(lds + kCtlBytes);
+  s.Linv = s.S + 36 * (N * (N + 1) / 2);
+  s.y = s.Linv + 36 * N;
+  return s;
+}
+
+// one BA call: setup + all iterations in one workgroup.  Thread 0 stamps
+// the 100 MHz wall clock after every phase (dpvo_ba_phase_marks).
+__device__ __forceinline__ void mark(const BaWs& w, int slot) {
+  if (threadIdx.x == 0 && slot < kMarks) w.tmark[slot] = (int64_t)wall_clock64();
+}
+
+__global__ void __launch_bounds__(kBaThreads)
+    ba_fused_kernel(BaArgs A, BaWs w, int P2, int iterations) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  mark(w, 0);
+  ba_setup_phase(A, w, lds, P2);
+  mark(w, 1);
+  const SolveLds L = solve_carve(lds, A.N);
+  for (int it = 0; it < iterations; it++) {
+    const int m0 = 2 + 5 * it;
+    ba_linearize_phase(A, w);
+    __syncthreads();
+    mark(w, m0);
+    ba_patch_phase(A, w);
+    __syncthreads();
+    mark(w, m0 + 1);
+    int fail = 0;
+    if (A.N > 0) {
+      ba_schur_phase(w, A.N, L.S, L.y);
+      __syncthreads();
+      mark(w, m0 + 2);
+      ba_solve_phase(A.N, L.S, L.Linv, L.y, L.ctl + 1);
+      fail = L.ctl[1];
+    }
+    mark(w, m0 + 3);
+    ba_update_phase(A, w, L.y, fail, nullptr);
+    __syncthreads();
+    mark(w, m0 + 4);
+  }
+}
+
+__global__ void __launch_bounds__(kBaThreads) ba_setup_kernel(BaArgs A, BaWs w, int P2) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  ba_setup_phase(A, w, lds, P2);
+}
+
+__global__ void __launch_bounds__(kBaThreads)
+    ba_build_kernel(BaArgs A, BaWs w, double* S_out, double* y_out) {
+  ba_linearize_phase(A, w);
+  __syncthreads();
+  ba_patch_phase(A, w);
+  __syncthreads();
+  if (A.N > 0) ba_schur_phase(w, A.N, S_out, y_out);
+}
+
+__global__ void __launch_bounds__(kBaThreads)
+    ba_solve_kernel(BaArgs A, BaWs w, const double* S_in, const double* y_in, double* dX_out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const SolveLds L = solve_carve(lds, A.N);
+  const int N = A.N, NL = N * (N + 1) / 2;
+  int fail = 0;
+  if (N > 0) {
+    for (int t = threadIdx.x; t < 36 * NL; t += blockDim.x) L.S[t] = S_in[t];
+    for (int t = threadIdx.x; t < 6 * N; t += blockDim.x) L.y[t] = y_in[t];
+    __syncthreads();
+    ba_solve_phase(N, L.S, L.Linv, L.y, L.ctl + 1);
+    fail = L.ctl[1];
+  }
+  ba_update_phase(A, w, L.y, fail, dX_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -642,19 +1029,17 @@ __global__ void __launch_bounds__(256)
 
 using namespace dpvo;
 
-static size_t setup_smem(int P2) {
-  return sizeof(unsigned long long) * P2 + sizeof(int) * (kSetupThreads / 64 + 4);
-}
-
 // Kernels whose LDS exceeds the 64 KiB default opt in to the 160 KiB of a CU.
 static void ensure_lds_limits() {
   static bool done = false;
   if (done) return;
+  const int big = 160 * 1024;
+  (void)hipFuncSetAttribute((const void*)ba_fused_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, big);
   (void)hipFuncSetAttribute((const void*)ba_setup_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)setup_smem(kMaxSetupE));
+                            hipFuncAttributeMaxDynamicSharedMemorySize, big);
   (void)hipFuncSetAttribute((const void*)ba_solve_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_smem(kMaxFree));
+                            hipFuncAttributeMaxDynamicSharedMemorySize, big);
   done = true;
 }
 
@@ -662,6 +1047,29 @@ static int pow2_at_least(int v) {
   int p = 1;
   while (p < v) p <<= 1;
   return p;
+}
+
+static BaArgs make_args(float* poses, float* patches, const float* intrinsics, const float* target,
+                        const float* weight, const float* lmbda, const int64_t* ii,
+                        const int64_t* jj, const int64_t* kk, int E, int P, int num_poses,
+                        int num_patches, int t0, int t1) {
+  BaArgs a;
+  a.poses = poses;
+  a.patches = patches;
+  a.intrinsics = intrinsics;
+  a.target = target;
+  a.weight = weight;
+  a.lmbda = lmbda;
+  a.ii = ii;
+  a.jj = jj;
+  a.kk = kk;
+  a.E = E;
+  a.P = P;
+  a.num_poses = num_poses;
+  a.num_patches = num_patches;
+  a.t0 = t0;
+  a.N = t1 - t0;
+  return a;
 }
 
 DPVO_EXPORT size_t dpvo_ba_workspace_bytes(int E, int t0, int t1) {
@@ -683,8 +1091,10 @@ DPVO_EXPORT int dpvo_ba_setup(const int64_t* ii, const int64_t* jj, const int64_
   ba_layout(E, N, (char*)workspace, &w);
   ensure_lds_limits();
   const int P2 = pow2_at_least(E < 2 ? 2 : E);
-  hipLaunchKernelGGL(ba_setup_kernel, dim3(1), dim3(kSetupThreads), setup_smem(P2),
-                     as_stream(stream), ii, jj, kk, E, num_patches, t0, N, P2, w);
+  BaArgs a = make_args(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ii, jj, kk, E, 0, 0,
+                       num_patches, t0, t1);
+  hipLaunchKernelGGL(ba_setup_kernel, dim3(1), dim3(kBaThreads), setup_lds(P2, N),
+                     as_stream(stream), a, w, P2);
   return launch_status();
 }
 
@@ -695,18 +1105,15 @@ DPVO_EXPORT int dpvo_ba_build_schur(const float* poses, const float* patches,
                                     int num_poses, int t0, int t1, void* workspace,
                                     double* S_lower, double* y, void* stream) {
   if (E <= 0) return DPVO_OK;
-  if (P < 2 || num_poses <= 0 || t1 < t0) return DPVO_ERR_INVALID;
+  if (P < 2 || num_poses <= 0 || t1 < t0 || !workspace) return DPVO_ERR_INVALID;
   const int N = t1 - t0;
   if (N > kMaxFree || E > kMaxSetupE) return DPVO_ERR_UNSUPPORTED;
   BaWs w;
   ba_layout(E, N, (char*)workspace, &w);
-  hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(ba_linearize_kernel, dim3((E + 255) / 256), dim3(256), 0, s, poses, patches,
-                     intrinsics, target, weight, lmbda, ii, jj, kk, P, num_poses, w);
-  int st = launch_status();
-  if (st || N == 0) return st;
-  const int NL = N * (N + 1) / 2;
-  hipLaunchKernelGGL(ba_schur_kernel, dim3(NL), dim3(kSchurThreads), 0, s, ii, jj, E, t0, N, w,
+  // kk is clamped against the patch count the setup recorded on the device
+  BaArgs a = make_args(const_cast<float*>(poses), const_cast<float*>(patches), intrinsics, target,
+                       weight, lmbda, ii, jj, kk, E, P, num_poses, 0, t0, t1);
+  hipLaunchKernelGGL(ba_build_kernel, dim3(1), dim3(kBaThreads), 0, as_stream(stream), a, w,
                      S_lower ? S_lower : w.S, y ? y : w.y);
   return launch_status();
 }
@@ -715,15 +1122,16 @@ DPVO_EXPORT int dpvo_ba_solve_update(float* poses, float* patches, const double*
                                      const double* y, int E, int P, int num_poses, int t0, int t1,
                                      void* workspace, double* dX_out, void* stream) {
   if (E <= 0) return DPVO_OK;
-  if (P < 2 || t1 < t0) return DPVO_ERR_INVALID;
+  if (P < 2 || t1 < t0 || !workspace) return DPVO_ERR_INVALID;
   const int N = t1 - t0;
   if (N > kMaxFree) return DPVO_ERR_UNSUPPORTED;
   BaWs w;
   ba_layout(E, N, (char*)workspace, &w);
   ensure_lds_limits();
-  hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(kSolveThreads), solve_smem(N),
-                     as_stream(stream), poses, patches, P, num_poses, t0, N,
-                     S_lower ? S_lower : w.S, y ? y : w.y, w, dX_out);
+  BaArgs a = make_args(poses, patches, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, E, P, num_poses, 0, t0, t1);
+  hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(kBaThreads), solve_lds(N), as_stream(stream),
+                     a, w, S_lower ? S_lower : w.S, y ? y : w.y, dX_out);
   return launch_status();
 }
 
@@ -738,6 +1146,17 @@ DPVO_EXPORT int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1
              : DPVO_ERR_LAUNCH;
 }
 
+DPVO_EXPORT int dpvo_ba_phase_marks(const void* workspace, int E, int t0, int t1,
+                                    int64_t* out, void* stream) {
+  if (!workspace || !out || E <= 0) return DPVO_ERR_INVALID;
+  BaWs w;
+  ba_layout(E, t1 > t0 ? t1 - t0 : 0, (char*)workspace, &w);
+  return hipMemcpyAsync(out, w.tmark, sizeof(int64_t) * kMarks, hipMemcpyDeviceToDevice,
+                        as_stream(stream)) == hipSuccess
+             ? DPVO_OK
+             : DPVO_ERR_LAUNCH;
+}
+
 DPVO_EXPORT int dpvo_ba_forward(float* poses, float* patches, const float* intrinsics,
                                 const float* target, const float* weight, const float* lmbda,
                                 const int64_t* ii, const int64_t* jj, const int64_t* kk, int E,
@@ -747,17 +1166,22 @@ DPVO_EXPORT int dpvo_ba_forward(float* poses, float* patches, const float* intri
   (void)PPF;
   (void)eff_impl;  // one block-sparse implementation serves both reference paths
   if (E <= 0 || iterations <= 0) return DPVO_OK;
-  int st = dpvo_ba_setup(ii, jj, kk, E, num_patches, t0, t1, workspace, workspace_bytes, stream);
-  if (st) return st;
-  for (int it = 0; it < iterations; it++) {
-    st = dpvo_ba_build_schur(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
-                             num_poses, t0, t1, workspace, nullptr, nullptr, stream);
-    if (st) return st;
-    st = dpvo_ba_solve_update(poses, patches, nullptr, nullptr, E, P, num_poses, t0, t1,
-                              workspace, nullptr, stream);
-    if (st) return st;
-  }
-  return DPVO_OK;
+  if (P < 2 || num_poses <= 0 || num_patches <= 0 || t1 < t0 || !workspace || !poses ||
+      !patches || !intrinsics || !target || !weight || !lmbda || !ii || !jj || !kk)
+    return DPVO_ERR_INVALID;
+  const int N = t1 - t0;
+  if (E > kMaxSetupE || N > kMaxFree) return DPVO_ERR_UNSUPPORTED;
+  if (workspace_bytes < dpvo_ba_workspace_bytes(E, t0, t1)) return DPVO_ERR_WORKSPACE;
+  BaWs w;
+  ba_layout(E, N, (char*)workspace, &w);
+  ensure_lds_limits();
+  const int P2 = pow2_at_least(E < 2 ? 2 : E);
+  const size_t a = setup_lds(P2, N), b = solve_lds(N);
+  BaArgs args = make_args(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
+                          num_poses, num_patches, t0, t1);
+  hipLaunchKernelGGL(ba_fused_kernel, dim3(1), dim3(kBaThreads), (a > b ? a : b),
+                     as_stream(stream), args, w, P2, iterations);
+  return launch_status();
 }
 
 DPVO_EXPORT int dpvo_reproject(const float* poses, const float* patches, const float* intrinsics,

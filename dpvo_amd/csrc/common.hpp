@@ -65,6 +65,9 @@ __device__ __forceinline__ T wave_sum(T v) {
 }
 
 // --- fp32 SE3 primitives of ba_cuda.cu:36-174 (restated, device) ---------------
+// No FMA contraction here: the per-edge arithmetic then rounds exactly like the
+// C oracle (x86, no FMA), which keeps the parity tests tight.
+#pragma clang fp contract(off)
 __device__ __forceinline__ void actSO3(const float* q, const float* X, float* Y) {
   float uv[3];
   uv[0] = 2.0f * (q[1] * X[2] - q[2] * X[1]);
@@ -176,5 +179,7 @@ __device__ __forceinline__ void retrSE3(const float* xi, const float* t, const f
   t1[1] += dt[1];
   t1[2] += dt[2];
 }
+
+#pragma clang fp contract(fast)
 
 }  // namespace dpvo

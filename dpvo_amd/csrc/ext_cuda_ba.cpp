@@ -14,7 +14,7 @@ static torch::Tensor f32_contig(const torch::Tensor& t, const char* name) {
 }
 
 // ba.cpp:32-45 -> cuda_ba (ba_cuda.cu:433-582).  Mutates poses / patches.
-std::vector<torch::Tensor> ba_forward(torch::Tensor poses, torch::Tensor patches,
+static torch::Tensor ba_forward_ws(torch::Tensor poses, torch::Tensor patches,
                                       torch::Tensor intrinsics, torch::Tensor target,
                                       torch::Tensor weight, torch::Tensor lmbda, torch::Tensor ii,
                                       torch::Tensor jj, torch::Tensor kk, int PPF, int t0, int t1,
@@ -41,7 +41,7 @@ std::vector<torch::Tensor> ba_forward(torch::Tensor poses, torch::Tensor patches
   const int E = ii.numel();
   TORCH_CHECK(jj.numel() == E && kk.numel() == E, "ii, jj, kk must have equal length");
   TORCH_CHECK(target.numel() >= 2 * E && weight.numel() >= 2 * E, "target/weight must be [.., E, 2]");
-  if (E == 0 || iterations <= 0) return {};
+  if (E == 0 || iterations <= 0) return torch::Tensor();
   TORCH_CHECK(t1 - t0 <= dpvo_ba_max_free_poses(), "cuda_ba.forward: t1 - t0 = ", t1 - t0,
               " free poses exceeds this build's single-workgroup Schur solve (",
               dpvo_ba_max_free_poses(), ")");
@@ -55,7 +55,34 @@ std::vector<torch::Tensor> ba_forward(torch::Tensor poses, torch::Tensor patches
                                iterations, eff_impl ? 1 : 0, ws.data_ptr(), wsb,
                                current_stream()),
                "cuda_ba.forward");
+  return ws;
+}
+
+std::vector<torch::Tensor> ba_forward(torch::Tensor poses, torch::Tensor patches,
+                                      torch::Tensor intrinsics, torch::Tensor target,
+                                      torch::Tensor weight, torch::Tensor lmbda, torch::Tensor ii,
+                                      torch::Tensor jj, torch::Tensor kk, int PPF, int t0, int t1,
+                                      int iterations, bool eff_impl) {
+  ba_forward_ws(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, PPF, t0, t1,
+                iterations, eff_impl);
   return {};
+}
+
+// Same call; returns the fused kernel's 32 wall-clock marks (100 MHz ticks:
+// start, setup, then linearize/patch/schur/solve/update per iteration).
+torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
+                               torch::Tensor intrinsics, torch::Tensor target, torch::Tensor weight,
+                               torch::Tensor lmbda, torch::Tensor ii, torch::Tensor jj,
+                               torch::Tensor kk, int PPF, int t0, int t1, int iterations,
+                               bool eff_impl) {
+  auto ws = ba_forward_ws(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, PPF, t0,
+                          t1, iterations, eff_impl);
+  auto out = torch::zeros({32}, poses.options().dtype(torch::kInt64));
+  if (!ws.defined()) return out;
+  check_status(dpvo_ba_phase_marks(ws.data_ptr(), ii.numel(), t0, t1, out.data_ptr<int64_t>(),
+                                   current_stream()),
+               "cuda_ba.forward_marks");
+  return out;
 }
 
 // ba.cpp:47-53 -> cuda_reproject (ba_cuda.cu:585-616)
@@ -185,5 +212,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("solve_update", &ba_solve_update, "Cholesky solve + pose/patch retraction");
   m.def("last_status", &ba_last_status, "status word of the last BA on a workspace");
   m.def("max_free_poses", &dpvo_ba_max_free_poses);
+  m.def("forward_marks", &ba_forward_marks, "forward + per-phase wall-clock marks");
   m.attr("native_library") = dpvo_version();
 }

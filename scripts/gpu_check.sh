@@ -11,6 +11,7 @@ fatal() { case "$1" in 124|134|137|139|-6|-11) return 0;; *) return 1;; esac; }
 STEPS="${STEPS:-tests smoke bench prof}"
 for s in $STEPS; do
   case $s in
+    ba) timeout -k 10 240 python -m pytest tests/test_ba_gpu.py -q -rf > $OUT/ba_gpu.log 2>&1; rc=$?;;
     tests) timeout -k 10 900 python -m pytest tests -m gpu -q -rf > $OUT/pytest_gpu.log 2>&1; rc=$?;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?;;
     bench) timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; rc=$?;;
@@ -18,7 +19,7 @@ for s in $STEPS; do
     *) echo "unknown step $s"; rc=0;;
   esac
   echo "step $s rc=$rc"
-  tail -3 $OUT/*$s*.log 2>/dev/null | tail -3
+  tail -3 $OUT/*$s*.log 2>/dev/null | tail -3 || true
   if fatal $rc; then echo "fatal rc=$rc at $s; stopping"; exit $rc; fi
 done
 exit 0

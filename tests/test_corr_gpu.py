@@ -115,7 +115,10 @@ def test_forward_levels_equals_per_level_calls(cc, gpu):
     c1, = cc.forward(f1, lv1, co / 1, ii, jj, R)
     c2, = cc.forward(f1, lv2, co / 4, ii, jj, R)
     ref = torch.stack([c1, c2], -1).view(1, len(ii), -1)  # dpvo.py:465
-    assert torch.equal(fused, ref)
+    # same per-level arithmetic; allow only last-bit differences from code
+    # generation of the two launch shapes
+    err = (fused - ref).abs().max().item()
+    assert err <= 1e-6 * max(1.0, ref.abs().max().item()), err
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.float64])
@@ -137,7 +140,7 @@ def test_forward_empty(cc, gpu):
 
 @pytest.mark.parametrize("kw", [dict(), dict(spread=4.0), dict(R=1, M=9)])
 def test_backward_matches_oracle(cc, gpu, kw):
-    f1, f2, co, ii, jj, R = _case(6, M=19, C=32, **kw)
+    f1, f2, co, ii, jj, R = _case(6, **{**dict(M=19, C=32), **kw})
     Dp = 2 * R + 1
     G = np.random.default_rng(7).standard_normal((1, len(ii), Dp, Dp, 3, 3)).astype(np.float32)
     g1, g2 = cc.backward(_t(f1, gpu), _t(f2, gpu), _t(co, gpu), _t(ii, gpu), _t(jj, gpu),
