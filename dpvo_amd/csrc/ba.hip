@@ -7,24 +7,28 @@
 //   dX = chol_solve(S, y); dZ = Q (u - E^T dX); pose / patch retraction.
 //
 // MI355X design (DESIGN.md "F-BA").  A DPVO window is small (N <= 20 free
-// poses, a few thousand edges) and the reference spends its time in ~15
-// kernel launches, float atomics and a host-side Cholesky per iteration.
-// Here the whole BA call -- setup and every iteration -- is ONE workgroup of
-// 1024 threads on one CU, phases separated by barriers, no float atomics,
-// every reduction in a fixed order (bitwise deterministic):
-//   setup      sort kk in LDS (bitonic), unique/inverse, edges grouped by
-//              patch, per-patch free-pose bitmask + block offsets, per-pose
-//              edge lists and patch lists (counts matrix + one block scan).
-//   linearize  thread per edge: the fp32 edge math of the reference
-//              -> J (fp32) and the edge's E/C/u contributions (fp64).
+// poses, a few thousand edges): the reference spends its time in ~15 kernel
+// launches, float atomics and a host-side Cholesky per iteration.  Here a BA
+// call -- setup and every iteration -- is ONE workgroup of 1024 threads,
+// phases separated by barriers, no float atomics, every reduction in a fixed
+// order (bitwise deterministic).  On one CU the enemy is the chain of
+// DEPENDENT global loads (~1 us each under load), so the setup pays once to
+// make every later phase one or two loads deep:
+//   setup      sort (kk, edge) in LDS (bitonic) -> "sorted positions": edges
+//              grouped by patch.  Per position a record (edge, ii, jj, kk)
+//              and the pose-block slots of its two poses; per patch the free
+//              pose mask and block offsets; per pose the edge list and the
+//              patch list, each partitioned (wave ballots, stable) into exact
+//              per-pose-pair ranges for the off-diagonal Schur blocks.
+//   linearize  thread per position: the fp32 edge math of the reference
+//              -> J (fp32) and the edge's E/C/u terms (fp64), position order.
 //   patch      thread per patch: Q_u, U_u and the E column blocks c_{u,p}.
-//   schur      gather, one team of lanes per lower 6x6 block of S: the team
-//              walks only the edge/patch lists of its pose, reduces in
-//              registers + shuffles; S and y land in LDS.
-//   solve      damping, right-looking block Cholesky in LDS (6x6 diagonal
-//              blocks factored + inverted by one lane, look-ahead so the
-//              factor overlaps the trailing update), block substitutions
-//              in one wave.
+//   schur      gather, one wave per diagonal block, 16-lane teams per
+//              off-diagonal block, each walking exactly its list range;
+//              S (lower 6x6 blocks) and y land in LDS.
+//   solve      damping; one wave: right-looking block Cholesky in LDS, the
+//              6x6 pivot blocks factored across 36 lanes (rsq + Newton),
+//              panels by substitution; block forward/back substitution.
 //   update     pose retraction, dZ = Q (u - E^T dX), patch retraction.
 // The split (build_schur -> all-reduce(S,y) -> solve_update) runs the same
 // phases in three single-workgroup kernels: the edge-sharded multi-GPU form
@@ -34,36 +38,44 @@
 namespace dpvo {
 
 constexpr int kBaThreads = 1024;
+constexpr int kBaWaves = kBaThreads / 64;
 constexpr int kMaxSetupE = 16384;  // LDS: 16384 x 8 B sort keys = 128 KiB
 constexpr int kMaxFree = 20;       // lower blocks of S for N=20: 59 KiB of LDS
 constexpr int kPerThread = kMaxSetupE / kBaThreads;
 constexpr int kJStride = 32;       // floats per edge: w[2] r[2] Jz[2] Ji[2][6] Jj[2][6]
-constexpr int kEStride = 16;       // doubles per edge: Ei[6] Ej[6] C u
+constexpr int kEStride = 14;       // doubles per edge: Ei[6] Ej[6] C u
 constexpr int kCtlBytes = 512;     // LDS control words + scan scratch
 constexpr int kNoPose = 31;        // "other pose" code of an edge with one free end
-constexpr int kMarks = 32;         // start, setup, then 5 phases x up to 6 iterations
+constexpr int kMarks = 256;        // [0..37] phases, [38..39] clock, [40..] detailed trace
+constexpr int kPairStride = 32;    // row stride of the pair-offset tables
 
 struct BaWs {
-  int32_t* pedge;   // [E]   edges grouped by patch (ascending edge id within a patch)
-  int32_t* poff;    // [E+1] patch -> edge range
+  int4* srec;       // [E]   per sorted position: edge id, ii, jj (clamped), kk (clamped)
+  int32_t* eslot;   // [E]   per position: block slot of ii | slot of jj << 8 (0xff = fixed)
+  int32_t* poff;    // [E+1] patch -> position range
   int32_t* boff;    // [E+1] patch -> pose-block range
   int32_t* bpose;   // [2E]  free pose of each block (ascending per patch)
   uint32_t* pmask;  // [E]   free poses touched by each patch
   int32_t* eoff;    // [kMaxFree+1] pose -> range of elist
-  int32_t* elist;   // [2E]  per pose: (edge << 8) | (other pose << 2) | roles
+  int32_t* elist0;  // [2E]  scratch: per pose, position order
+  int32_t* elist;   // [2E]  per pose: (position << 8) | (other pose << 2) | roles,
+                    //       stable-partitioned: other = 0..a-1 first (pair ranges)
+  int32_t* epair;   // [kMaxFree][32] start of pair (a, b) in elist, b <= a ([a] = end)
   int32_t* qoff;    // [kMaxFree+1] pose -> range of qlist
-  int32_t* qlist;   // [2E]  per pose: patches touching it
+  int2* qlist;      // [2E]  per pose: (patch, its block index for this pose)
+  int32_t* qpair;   // [kMaxFree][32] start of pair (a, b) in qplist, b <= a ([a] = end)
+  int2* qplist;     // [E*(kMaxFree-1)] patches in a and b: (patch, blk_a | blk_b << 16)
   int32_t* meta;    // [8]   nuniq, status, nblocks, num_patches
   int64_t* kx;      // [E]   unique patch ids (ascending)
-  float* J;         // [E][32]
-  double* EC;       // [E][16]
+  float* J;         // [E][32]   by position
+  double* EC;       // [E][14]   by position
   double* Q;        // [E]
   double* U;        // [E]
   double* cb;       // [2E][6]
   double* S;        // [NL][36] (split API default)
   double* y;        // [6N]
   double* dX;       // [6N]
-  int64_t* tmark;   // [kMarks] wall-clock marks of the fused kernel's phases
+  int64_t* tmark;   // [kMarks]
 };
 
 struct BaArgs {
@@ -83,6 +95,7 @@ static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; 
 
 static size_t ba_layout(int E, int N, char* base, BaWs* w) {
   const size_t NL = (size_t)N * (N + 1) / 2;
+  const size_t npair = (size_t)E * (kMaxFree - 1);
   size_t off = 0;
   auto take = [&](size_t bytes) -> char* {
     char* p = base ? base + off : nullptr;
@@ -90,15 +103,20 @@ static size_t ba_layout(int E, int N, char* base, BaWs* w) {
     return p;
   };
   BaWs t;
-  t.pedge = (int32_t*)take(sizeof(int32_t) * E);
+  t.srec = (int4*)take(sizeof(int4) * E);
+  t.eslot = (int32_t*)take(sizeof(int32_t) * E);
   t.poff = (int32_t*)take(sizeof(int32_t) * (E + 1));
   t.boff = (int32_t*)take(sizeof(int32_t) * (E + 1));
   t.bpose = (int32_t*)take(sizeof(int32_t) * 2 * E);
   t.pmask = (uint32_t*)take(sizeof(uint32_t) * E);
   t.eoff = (int32_t*)take(sizeof(int32_t) * (kMaxFree + 1));
+  t.elist0 = (int32_t*)take(sizeof(int32_t) * 2 * E);
   t.elist = (int32_t*)take(sizeof(int32_t) * 2 * E);
+  t.epair = (int32_t*)take(sizeof(int32_t) * kMaxFree * kPairStride);
   t.qoff = (int32_t*)take(sizeof(int32_t) * (kMaxFree + 1));
-  t.qlist = (int32_t*)take(sizeof(int32_t) * 2 * E);
+  t.qlist = (int2*)take(sizeof(int2) * 2 * E);
+  t.qpair = (int32_t*)take(sizeof(int32_t) * kMaxFree * kPairStride);
+  t.qplist = (int2*)take(sizeof(int2) * npair);
   t.meta = (int32_t*)take(sizeof(int32_t) * 8);
   t.kx = (int64_t*)take(sizeof(int64_t) * E);
   t.J = (float*)take(sizeof(float) * kJStride * E);
@@ -114,15 +132,16 @@ static size_t ba_layout(int E, int N, char* base, BaWs* w) {
   return off;
 }
 
-// LDS bytes of each phase group (all LDS is dynamic, carved from one base).
+// LDS of the setup: [ctl][keys 8*P2] aliased after the sort by
+// [pij: 4*P2][work: 4*max(P2, N*T)]
 static size_t setup_lds(int P2, int N) {
-  const size_t ints = (size_t)(P2 > N * kBaThreads ? P2 : N * kBaThreads);
-  const size_t a = sizeof(unsigned long long) * (size_t)P2, b = sizeof(int) * ints;
+  const size_t work = (size_t)(P2 > N * kBaThreads ? P2 : N * kBaThreads);
+  const size_t a = 8 * (size_t)P2, b = 4 * (size_t)P2 + 4 * work;
   return kCtlBytes + (a > b ? a : b);
 }
 static size_t solve_lds(int N) {
   const size_t NL = (size_t)N * (N + 1) / 2;
-  return kCtlBytes + sizeof(double) * (36 * NL + 36 * (size_t)N + 6 * (size_t)N);
+  return kCtlBytes + sizeof(double) * (36 * NL + 6 * (size_t)N + 6 * (size_t)N);
 }
 
 __device__ __forceinline__ int tri_row(int t) {  // a with a(a+1)/2 <= t < (a+1)(a+2)/2
@@ -132,6 +151,15 @@ __device__ __forceinline__ int tri_row(int t) {  // a with a(a+1)/2 <= t < (a+1)
   return r;
 }
 __device__ __forceinline__ int blk(int a, int b) { return a * (a + 1) / 2 + b; }  // a >= b
+__device__ __forceinline__ bool is_free(int64_t p, int N) { return p >= 0 && p < N; }
+__device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
+  return (1ull << lane) - 1ull;
+}
+
+// wall-clock trace stamp by thread 0 (slot < kMarks; tmark may be null)
+__device__ __forceinline__ void trace(int64_t* tmark, int slot) {
+  if (tmark && threadIdx.x == 0 && slot < kMarks) tmark[slot] = (int64_t)wall_clock64();
+}
 
 // ---------------------------------------------------------------------------
 // block-wide exclusive scan of data[0..n) in LDS (int), returns the total.
@@ -173,19 +201,29 @@ __device__ int block_exclusive_scan(int* data, int n, int* scratch) {
   return total;
 }
 
-__device__ __forceinline__ bool is_free(int64_t p, int N) { return p >= 0 && p < N; }
+// exclusive scan over the 64 lanes of a wave
+__device__ __forceinline__ int wave_exclusive_scan(int v, int lane) {
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(x, o, 64);
+    if (lane >= o) x += t;
+  }
+  return x - v;
+}
 
 // ---------------------------------------------------------------------------
 // SETUP: unique/inverse of kk (torch::_unique(kk, sorted, inverse),
 // ba_cuda.cu:447) and the sparse structure every later phase walks.
 // ---------------------------------------------------------------------------
 __device__ void ba_setup_phase(const BaArgs& A, const BaWs& w, char* lds, int P2) {
-  const int tid = threadIdx.x, T = blockDim.x;
+  const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wid = tid >> 6;
   const int E = A.E, N = A.N, t0 = A.t0;
   int* ctl = reinterpret_cast<int*>(lds);  // [0] bad kk
   int* scr = ctl + 64;                     // scan scratch (T/64 + 1)
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(lds + kCtlBytes);
-  int* ints = reinterpret_cast<int*>(lds + kCtlBytes);  // aliases keys once they are consumed
+  int* pij = reinterpret_cast<int*>(lds + kCtlBytes);         // after the sort
+  int* work = reinterpret_cast<int*>(lds + kCtlBytes) + P2;   // after the sort
   if (tid == 0) ctl[0] = 0;
   __syncthreads();
   for (int i = tid; i < P2; i += T) {
@@ -216,7 +254,9 @@ __device__ void ba_setup_phase(const BaArgs& A, const BaWs& w, char* lds, int P2
       __syncthreads();
     }
   }
-  // heads of equal-kk runs, kept in registers while the keys region is reused
+  trace(w.tmark, 40);
+  // sorted position i: edge pe, patch id kv, head-of-run flag hd (registers
+  // while the key region is reused)
   int pe[kPerThread], kv[kPerThread], hd[kPerThread];
 #pragma unroll
   for (int k = 0; k < kPerThread; k++) {
@@ -233,20 +273,27 @@ __device__ void ba_setup_phase(const BaArgs& A, const BaWs& w, char* lds, int P2
 #pragma unroll
   for (int k = 0; k < kPerThread; k++) {
     const int i = tid + k * T;
-    if (i < E) ints[i] = hd[k];
+    if (i < E) {
+      const int e = pe[k];
+      const int64_t gi = A.ii[e], gj = A.jj[e];
+      const int64_t pi = gi - t0, pj = gj - t0;
+      const int ci = is_free(pi, N) ? (int)pi : kNoPose, cj = is_free(pj, N) ? (int)pj : kNoPose;
+      pij[i] = ci | (cj << 8);
+      work[i] = hd[k];
+      const int ix = (int)min(max(gi, (int64_t)0), (int64_t)A.num_poses - 1);
+      const int jx = (int)min(max(gj, (int64_t)0), (int64_t)A.num_poses - 1);
+      w.srec[i] = make_int4(e, ix, jx, kv[k]);
+    }
   }
   __syncthreads();
-  const int nuniq = block_exclusive_scan(ints, E, scr);
+  const int nuniq = block_exclusive_scan(work, E, scr);
 #pragma unroll
   for (int k = 0; k < kPerThread; k++) {
     const int i = tid + k * T;
-    if (i < E) {
-      w.pedge[i] = pe[k];
-      if (hd[k]) {
-        const int r = ints[i];
-        w.kx[r] = kv[k];
-        w.poff[r] = i;
-      }
+    if (i < E && hd[k]) {
+      const int r = work[i];
+      w.kx[r] = kv[k];
+      w.poff[r] = i;
     }
   }
   if (tid == 0) {
@@ -256,27 +303,33 @@ __device__ void ba_setup_phase(const BaArgs& A, const BaWs& w, char* lds, int P2
     w.meta[3] = A.num_patches;
   }
   __syncthreads();
-  // per-patch free-pose masks (N <= 20 < 32) and pose-block offsets
+  trace(w.tmark, 41);
+  // per patch: free-pose mask, block count -> block offsets, per-position slots
   for (int u = tid; u < nuniq; u += T) {
     unsigned mask = 0;
     for (int t = w.poff[u]; t < w.poff[u + 1]; t++) {
-      const int e = w.pedge[t];
-      const int64_t pi = A.ii[e] - t0, pj = A.jj[e] - t0;
-      if (is_free(pi, N)) mask |= 1u << pi;
-      if (is_free(pj, N)) mask |= 1u << pj;
+      const int c = pij[t];
+      if ((c & 0xff) != kNoPose) mask |= 1u << (c & 0xff);
+      if ((c >> 8) != kNoPose) mask |= 1u << (c >> 8);
     }
     w.pmask[u] = mask;
-    ints[u] = __popc(mask);
+    work[u] = __popc(mask);
   }
   __syncthreads();
-  const int nblocks = block_exclusive_scan(ints, nuniq, scr);
+  const int nblocks = block_exclusive_scan(work, nuniq, scr);
   for (int u = tid; u < nuniq; u += T) {
-    const int base = ints[u];
+    const int base = work[u];
     const unsigned mask = w.pmask[u];
     w.boff[u] = base;
     for (unsigned m = mask; m; m &= m - 1) {
       const int p = __ffs(m) - 1;
       w.bpose[base + __popc(mask & ((1u << p) - 1u))] = p;
+    }
+    for (int t = w.poff[u]; t < w.poff[u + 1]; t++) {
+      const int c = pij[t], ci = c & 0xff, cj = c >> 8;
+      const int si = ci != kNoPose ? __popc(mask & ((1u << ci) - 1u)) : 0xff;
+      const int sj = cj != kNoPose ? __popc(mask & ((1u << cj) - 1u)) : 0xff;
+      w.eslot[t] = si | (sj << 8);
     }
   }
   if (tid == 0) {
@@ -284,59 +337,147 @@ __device__ void ba_setup_phase(const BaArgs& A, const BaWs& w, char* lds, int P2
     w.meta[2] = nblocks;
   }
   if (N == 0) {
-    if (tid == 0) w.eoff[0] = w.qoff[0] = 0;
     __syncthreads();
     return;
   }
   __syncthreads();
-  // per-pose edge lists: counts matrix [pose][thread] over contiguous edge
-  // chunks, one scan, then every thread fills its own cells (ascending edges)
+  trace(w.tmark, 42);
+  // per-pose edge lists (position order): counts matrix [pose][thread] over
+  // contiguous position chunks, one scan, every thread fills its own cells
   const int ch = (E + T - 1) / T, elo = min(tid * ch, E), ehi = min(elo + ch, E);
-  for (int p = 0; p < N; p++) ints[p * T + tid] = 0;
-  for (int e = elo; e < ehi; e++) {
-    const int64_t pi = A.ii[e] - t0, pj = A.jj[e] - t0;
-    if (is_free(pi, N)) ints[pi * T + tid]++;
-    if (is_free(pj, N) && pj != pi) ints[pj * T + tid]++;
+  for (int p = 0; p < N; p++) work[p * T + tid] = 0;
+  for (int t = elo; t < ehi; t++) {
+    const int c = pij[t], ci = c & 0xff, cj = c >> 8;
+    if (ci != kNoPose) work[ci * T + tid]++;
+    if (cj != kNoPose && cj != ci) work[cj * T + tid]++;
   }
   __syncthreads();
-  int total = block_exclusive_scan(ints, N * T, scr);
-  if (tid < N) w.eoff[tid] = ints[tid * T];
+  int total = block_exclusive_scan(work, N * T, scr);
+  if (tid < N) w.eoff[tid] = work[tid * T];
   if (tid == 0) w.eoff[N] = total;
   __syncthreads();
-  for (int e = elo; e < ehi; e++) {
-    const int64_t pi = A.ii[e] - t0, pj = A.jj[e] - t0;
-    const bool fi = is_free(pi, N), fj = is_free(pj, N);
-    if (fi) {
-      const int roles = 1 | ((pj == pi) ? 2 : 0);
-      const int other = (fj && pj != pi) ? (int)pj : kNoPose;
-      w.elist[ints[pi * T + tid]++] = (e << 8) | (other << 2) | roles;
+  for (int t = elo; t < ehi; t++) {
+    const int c = pij[t], ci = c & 0xff, cj = c >> 8;
+    if (ci != kNoPose) {
+      const int roles = 1 | ((cj == ci) ? 2 : 0);
+      const int other = (cj != ci) ? cj : kNoPose;
+      w.elist0[work[ci * T + tid]++] = (t << 8) | (other << 2) | roles;
     }
-    if (fj && pj != pi) {
-      const int other = fi ? (int)pi : kNoPose;
-      w.elist[ints[pj * T + tid]++] = (e << 8) | (other << 2) | 2;
+    if (cj != kNoPose && cj != ci) w.elist0[work[cj * T + tid]++] = (t << 8) | (ci << 2) | 2;
+  }
+  __syncthreads();
+  trace(w.tmark, 43);
+  // per-pose patch lists (patch order), same construction
+  const int cu = (nuniq + T - 1) / T, ulo = min(tid * cu, nuniq), uhi = min(ulo + cu, nuniq);
+  for (int p = 0; p < N; p++) work[p * T + tid] = 0;
+  for (int u = ulo; u < uhi; u++)
+    for (unsigned m = w.pmask[u]; m; m &= m - 1) work[(__ffs(m) - 1) * T + tid]++;
+  __syncthreads();
+  total = block_exclusive_scan(work, N * T, scr);
+  if (tid < N) w.qoff[tid] = work[tid * T];
+  if (tid == 0) w.qoff[N] = total;
+  __syncthreads();
+  for (int u = ulo; u < uhi; u++) {
+    const unsigned mask = w.pmask[u];
+    const int b0 = w.boff[u];
+    for (unsigned m = mask; m; m &= m - 1) {
+      const int p = __ffs(m) - 1;
+      w.qlist[work[p * T + tid]++] = make_int2(u, b0 + __popc(mask & ((1u << p) - 1u)));
     }
   }
   __syncthreads();
-  // per-pose patch lists, same construction over patch chunks
-  const int cu = (nuniq + T - 1) / T, ulo = min(tid * cu, nuniq), uhi = min(ulo + cu, nuniq);
-  for (int p = 0; p < N; p++) ints[p * T + tid] = 0;
-  for (int u = ulo; u < uhi; u++)
-    for (unsigned m = w.pmask[u]; m; m &= m - 1) ints[(__ffs(m) - 1) * T + tid]++;
+  trace(w.tmark, 44);
+  // pair ranges: one wave per pose a; stable partition of elist(a) by the
+  // other pose b < a (bucket a = "rest"), and of qlist(a) into one range per
+  // b < a of the patches that also touch b.  Wave ballots: deterministic.
+  for (int a = wid; a < N; a += kBaWaves) {
+    const int s0 = w.eoff[a], s1 = w.eoff[a + 1];
+    int cnt = 0;  // lane b: entries with other == b (lane a: the rest)
+    for (int base = s0; base < s1; base += 64) {
+      const int t = base + lane;
+      int o = (t < s1) ? ((w.elist0[t] >> 2) & 31) : -1;
+      if (t < s1 && o >= a) o = a;
+      for (int b = 0; b <= a; b++) {
+        const unsigned long long m = __ballot(o == b);
+        if (lane == b) cnt += __popcll(m);
+      }
+    }
+    int cur = s0 + wave_exclusive_scan(lane <= a ? cnt : 0, lane);
+    if (lane <= a) w.epair[a * kPairStride + lane] = cur;
+    for (int base = s0; base < s1; base += 64) {
+      const int t = base + lane;
+      const int ent = (t < s1) ? w.elist0[t] : 0;
+      int o = (t < s1) ? ((ent >> 2) & 31) : -1;
+      if (t < s1 && o >= a) o = a;
+      for (int b = 0; b <= a; b++) {
+        const unsigned long long m = __ballot(o == b);
+        if (m) {
+          const int pos = __shfl(cur, b, 64);
+          if (o == b) w.elist[pos + __popcll(m & lanemask_lt(lane))] = ent;
+          if (lane == b) cur += __popcll(m);
+        }
+      }
+    }
+  }
+  // qplist: a patch of qlist(a) lands in the range of every b < a in its mask
+  if (tid == 0) ctl[1] = 0;
   __syncthreads();
-  total = block_exclusive_scan(ints, N * T, scr);
-  if (tid < N) w.qoff[tid] = ints[tid * T];
-  if (tid == 0) w.qoff[N] = total;
+  trace(w.tmark, 45);
+  for (int a = wid; a < N; a += kBaWaves) {  // sizes first: ranges of all poses are stacked
+    const int s0 = w.qoff[a], s1 = w.qoff[a + 1];
+    int cnt = 0;
+    for (int base = s0; base < s1; base += 64) {
+      const int t = base + lane;
+      const unsigned mask = (t < s1) ? w.pmask[w.qlist[t].x] : 0u;
+      for (int b = 0; b < a; b++) {
+        const unsigned long long m = __ballot((mask >> b) & 1u);
+        if (lane == b) cnt += __popcll(m);
+      }
+    }
+    int tot = cnt;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    if (lane == 0) work[a] = tot;
+    if (lane < a) work[kMaxFree + a * kPairStride + lane] = cnt;
+  }
   __syncthreads();
-  for (int u = ulo; u < uhi; u++)
-    for (unsigned m = w.pmask[u]; m; m &= m - 1) w.qlist[ints[(__ffs(m) - 1) * T + tid]++] = u;
+  if (tid < 64) {  // stack the per-pose ranges (poses in order)
+    int base = 0;
+    for (int a = 0; a < N; a++) {
+      const int c = (lane < a) ? work[kMaxFree + a * kPairStride + lane] : 0;
+      const int ex = wave_exclusive_scan(c, lane);
+      if (lane < a) work[kMaxFree + a * kPairStride + lane] = base + ex;
+      if (lane == 0) w.qpair[a * kPairStride + a] = base + work[a];
+      base += work[a];
+    }
+  }
+  __syncthreads();
+  for (int a = wid; a < N; a += kBaWaves) {
+    const int s0 = w.qoff[a], s1 = w.qoff[a + 1];
+    int cur = (lane < a) ? work[kMaxFree + a * kPairStride + lane] : 0;
+    if (lane < a) w.qpair[a * kPairStride + lane] = cur;
+    for (int base = s0; base < s1; base += 64) {
+      const int t = base + lane;
+      const int2 q = (t < s1) ? w.qlist[t] : make_int2(0, 0);
+      const unsigned mask = (t < s1) ? w.pmask[q.x] : 0u;
+      const int b0 = (t < s1) ? w.boff[q.x] : 0;
+      for (int b = 0; b < a; b++) {
+        const bool in = (mask >> b) & 1u;
+        const unsigned long long m = __ballot(in);
+        if (m) {
+          const int pos = __shfl(cur, b, 64);
+          if (in) {
+            const int sb = b0 + __popc(mask & ((1u << b) - 1u));
+            w.qplist[pos + __popcll(m & lanemask_lt(lane))] = make_int2(q.x, q.y | (sb << 16));
+          }
+          if (lane == b) cur += __popcll(m);
+        }
+      }
+    }
+  }
   __syncthreads();
 }
 
-// ---------------------------------------------------------------------------
-// LINEARIZE: fp32 edge math exactly as reprojection_residuals_and_hessian
-// (ba_cuda.cu:265-333), contraction off so it rounds like the reference's
-// source order; then the edge's E blocks, C and u terms in fp64.
-// ---------------------------------------------------------------------------
 #pragma clang fp contract(off)
 __device__ __forceinline__ void edge_linearize(const float* poses, const float* patches, int P,
                                                float fx, float fy, float cx, float cy, float tx,
@@ -420,18 +561,24 @@ __global__ void reproject_kernel(const float* __restrict__ poses, const float* _
 }
 #pragma clang fp contract(fast)
 
-__device__ void ba_linearize_phase(const BaArgs& A, const BaWs& w) {
-  const float fx = A.intrinsics[0], fy = A.intrinsics[1], cx = A.intrinsics[2],
-              cy = A.intrinsics[3];
-  const int64_t kmax = (int64_t)w.meta[3] - 1;  // patch count recorded by the setup
-  for (int e = threadIdx.x; e < A.E; e += blockDim.x) {
-    const int ix = (int)min(max(A.ii[e], (int64_t)0), (int64_t)A.num_poses - 1);
-    const int jx = (int)min(max(A.jj[e], (int64_t)0), (int64_t)A.num_poses - 1);
-    const int64_t kx = min(max(A.kk[e], (int64_t)0), kmax);  // memory guard (reference: unchecked)
+// linearize: thread per sorted position.  The restrict-qualified helper lets
+// the loads of both positions a thread owns issue before any store.
+__device__ __forceinline__ void linearize_positions(
+    const float* __restrict__ poses, const float* __restrict__ patches,
+    const float* __restrict__ intrinsics, const float* __restrict__ target,
+    const float* __restrict__ weight, const int4* __restrict__ srec, int E, int P, int kmax,
+    float* __restrict__ J, double* __restrict__ EC) {
+  const float fx = intrinsics[0], fy = intrinsics[1], cx = intrinsics[2], cy = intrinsics[3];
+#pragma unroll 2
+  for (int i = threadIdx.x; i < E; i += blockDim.x) {
+    const int4 r = srec[i];
+    const int e = r.x;
+    const int64_t kx = min(r.w, kmax);  // memory guard (reference: unchecked)
+    const float2 tg = reinterpret_cast<const float2*>(target)[e];
+    const float2 wt = reinterpret_cast<const float2*>(weight)[e];
     float o[30];
-    edge_linearize(A.poses, A.patches, A.P, fx, fy, cx, cy, A.target[2 * e], A.target[2 * e + 1],
-                   A.weight[2 * e], A.weight[2 * e + 1], ix, jx, kx, o);
-    float4* Jo = reinterpret_cast<float4*>(w.J + (size_t)kJStride * e);
+    edge_linearize(poses, patches, P, fx, fy, cx, cy, tg.x, tg.y, wt.x, wt.y, r.y, r.z, kx, o);
+    float4* Jo = reinterpret_cast<float4*>(J + (size_t)kJStride * i);
 #pragma unroll
     for (int k = 0; k < 7; k++) Jo[k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
     reinterpret_cast<float2*>(Jo + 7)[0] = make_float2(o[28], o[29]);
@@ -441,7 +588,7 @@ __device__ void ba_linearize_phase(const BaArgs& A, const BaWs& w) {
 #pragma unroll
     for (int row = 0; row < 2; row++) {  // ba_cuda.cu:352-373
       const double wr = o[row];
-      const float r = o[2 + row], Jz = o[4 + row];
+      const float rr = o[2 + row], Jz = o[4 + row];
       const double wz = wr * Jz;
 #pragma unroll
       for (int k = 0; k < 6; k++) {
@@ -449,67 +596,100 @@ __device__ void ba_linearize_phase(const BaArgs& A, const BaWs& w) {
         ec[6 + k] += wz * o[18 + 6 * row + k];
       }
       ec[12] += wz * Jz;
-      ec[13] += wr * r * Jz;
+      ec[13] += wr * rr * Jz;
     }
-    double2* Eo = reinterpret_cast<double2*>(w.EC + (size_t)kEStride * e);
+    double2* Eo = reinterpret_cast<double2*>(EC + (size_t)kEStride * i);
 #pragma unroll
     for (int k = 0; k < 7; k++) Eo[k] = make_double2(ec[2 * k], ec[2 * k + 1]);
   }
 }
 
+__device__ void ba_linearize_phase(const BaArgs& A, const BaWs& w) {
+  linearize_positions(A.poses, A.patches, A.intrinsics, A.target, A.weight, w.srec, A.E, A.P,
+                      w.meta[3] - 1, w.J, w.EC);
+}
+
 // ---------------------------------------------------------------------------
 // PATCH: Q_u = 1/(C_u + lmbda), U_u, and c_{u,p} = sum of the E blocks of
-// pose p over the patch's edges (ascending edge order).
+// pose p over the patch's edges (position = ascending edge order).
 // ---------------------------------------------------------------------------
-__device__ void ba_patch_phase(const BaArgs& A, const BaWs& w) {
-  const double lam = (double)A.lmbda[0];
-  const int nuniq = w.meta[0];
+constexpr int kRegBlocks = 4;  // patches with <= 4 pose blocks accumulate in registers
+
+__device__ __forceinline__ void patch_sums(const int32_t* __restrict__ poff,
+                                           const int32_t* __restrict__ boff,
+                                           const int32_t* __restrict__ eslot,
+                                           const double* __restrict__ EC, double lam, int nuniq,
+                                           double* __restrict__ Q, double* __restrict__ U,
+                                           double* __restrict__ cb) {
   for (int u = threadIdx.x; u < nuniq; u += blockDim.x) {
-    const int a = w.poff[u], b = w.poff[u + 1];
-    double C = 0.0, Uu = 0.0;
+    const int a = poff[u], b = poff[u + 1];
+    const int s0 = boff[u], nb = boff[u + 1] - s0;
+    double C = 0.0, Uu = 0.0, c[kRegBlocks][6];
+#pragma unroll
+    for (int s = 0; s < kRegBlocks; s++)
+#pragma unroll
+      for (int k = 0; k < 6; k++) c[s][k] = 0.0;
     for (int t = a; t < b; t++) {
-      const double* ec = w.EC + (size_t)kEStride * w.pedge[t];
+      const double2* ep = reinterpret_cast<const double2*>(EC + (size_t)kEStride * t);
+      double ec[14];
+#pragma unroll
+      for (int k = 0; k < 7; k++) {
+        const double2 v = ep[k];
+        ec[2 * k] = v.x;
+        ec[2 * k + 1] = v.y;
+      }
+      const int sl = eslot[t], si = sl & 0xff, sj = sl >> 8;
       C += ec[12];
       Uu += ec[13];
-    }
-    w.Q[u] = 1.0 / (C + lam);  // ba_cuda.cu:519
-    w.U[u] = Uu;
-    for (int s = w.boff[u]; s < w.boff[u + 1]; s++) {
-      const int p = w.bpose[s];
-      double c[6] = {0, 0, 0, 0, 0, 0};
-      for (int t = a; t < b; t++) {
-        const int e = w.pedge[t];
-        const double* ec = w.EC + (size_t)kEStride * e;
-        const int64_t pi = A.ii[e] - A.t0, pj = A.jj[e] - A.t0;
-        if (pi == p)
 #pragma unroll
-          for (int k = 0; k < 6; k++) c[k] += ec[k];
-        if (pj == p)
+      for (int s = 0; s < kRegBlocks; s++) {
+        if (si == s)
 #pragma unroll
-          for (int k = 0; k < 6; k++) c[k] += ec[6 + k];
+          for (int k = 0; k < 6; k++) c[s][k] += ec[k];
+        if (sj == s)
+#pragma unroll
+          for (int k = 0; k < 6; k++) c[s][k] += ec[6 + k];
       }
-      double2* co = reinterpret_cast<double2*>(w.cb + 6 * (size_t)s);
-      co[0] = make_double2(c[0], c[1]);
-      co[1] = make_double2(c[2], c[3]);
-      co[2] = make_double2(c[4], c[5]);
+    }
+    Q[u] = 1.0 / (C + lam);  // ba_cuda.cu:519
+    U[u] = Uu;
+    if (nb <= kRegBlocks) {
+#pragma unroll
+      for (int s = 0; s < kRegBlocks; s++) {
+        if (s < nb) {
+          double2* co = reinterpret_cast<double2*>(cb + 6 * (size_t)(s0 + s));
+          co[0] = make_double2(c[s][0], c[s][1]);
+          co[1] = make_double2(c[s][2], c[s][3]);
+          co[2] = make_double2(c[s][4], c[s][5]);
+        }
+      }
+    } else {
+      for (int s = 0; s < nb; s++) {  // rare: many poses on one patch
+        double cs[6] = {0, 0, 0, 0, 0, 0};
+        for (int t = a; t < b; t++) {
+          const double* ec = EC + (size_t)kEStride * t;
+          const int sl = eslot[t];
+          if ((sl & 0xff) == s)
+#pragma unroll
+            for (int k = 0; k < 6; k++) cs[k] += ec[k];
+          if ((sl >> 8) == s)
+#pragma unroll
+            for (int k = 0; k < 6; k++) cs[k] += ec[6 + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) cb[6 * (size_t)(s0 + s) + k] = cs[k];
+      }
     }
   }
+}
+
+__device__ void ba_patch_phase(const BaArgs& A, const BaWs& w) {
+  patch_sums(w.poff, w.boff, w.eslot, w.EC, (double)A.lmbda[0], w.meta[0], w.Q, w.U, w.cb);
 }
 
 // ---------------------------------------------------------------------------
 // SCHUR: S = B - E Q E^T (lower 6x6 blocks), y = v - E Q u.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void load_row(const float* o, int row, double& wr, float& r, float* ji,
-                                         float* jv) {
-  wr = o[row];
-  r = o[2 + row];
-#pragma unroll
-  for (int k = 0; k < 6; k++) {
-    ji[k] = o[6 + 6 * row + k];
-    jv[k] = o[18 + 6 * row + k];
-  }
-}
-
 template <int NV>
 __device__ __forceinline__ void team_reduce(double* v, int tau) {
   for (int o = tau >> 1; o > 0; o >>= 1)
@@ -517,24 +697,39 @@ __device__ __forceinline__ void team_reduce(double* v, int tau) {
     for (int i = 0; i < NV; i++) v[i] += __shfl_xor(v[i], o, 64);
 }
 
-// diagonal block (a, a) and y_a; team of tau lanes (tau | 64)
-__device__ void schur_diag(const BaWs& w, int a, int lane, int tau, double* Sout, double* yout) {
+// diagonal block (a, a) and y_a; a full wave
+__device__ __forceinline__ void schur_diag(const int32_t* __restrict__ elist,
+                                           const int2* __restrict__ qlist,
+                                           const float* __restrict__ J,
+                                           const double* __restrict__ Q,
+                                           const double* __restrict__ U,
+                                           const double* __restrict__ cb, int e0, int e1, int q0,
+                                           int q1, int lane, double* Sb, double* ya) {
   double acc[21], yv[6];
 #pragma unroll
   for (int i = 0; i < 21; i++) acc[i] = 0.0;
 #pragma unroll
   for (int i = 0; i < 6; i++) yv[i] = 0.0;
-  const int e1 = w.eoff[a + 1];
-  for (int t = w.eoff[a] + lane; t < e1; t += tau) {  // B_aa, v_a (ba_cuda.cu:339-370)
-    const int ent = w.elist[t];
+#pragma unroll 2
+  for (int t = e0 + lane; t < e1; t += 64) {  // B_aa, v_a (ba_cuda.cu:339-370)
+    const int ent = elist[t];
     const int roles = ent & 3;
-    const float* o = w.J + (size_t)kJStride * (ent >> 8);
+    const float4* o4 = reinterpret_cast<const float4*>(J + (size_t)kJStride * (ent >> 8));
+    float o[32];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const float4 v = o4[k];
+      o[4 * k] = v.x;
+      o[4 * k + 1] = v.y;
+      o[4 * k + 2] = v.z;
+      o[4 * k + 3] = v.w;
+    }
 #pragma unroll
     for (int row = 0; row < 2; row++) {
-      double wr;
-      float r, ji[6], jv[6];
-      load_row(o, row, wr, r, ji, jv);
-      const double wrr = wr * r;
+      const double wr = o[row];
+      const double wrr = wr * o[2 + row];
+      const float* ji = o + 6 + 6 * row;
+      const float* jv = o + 18 + 6 * row;
       if (roles & 1) {
 #pragma unroll
         for (int x = 0, q = 0; x < 6; x++) {
@@ -561,15 +756,13 @@ __device__ void schur_diag(const BaWs& w, int a, int lane, int tau, double* Sout
       }
     }
   }
-  const int q1 = w.qoff[a + 1];
-  for (int t = w.qoff[a] + lane; t < q1; t += tau) {  // E Q E^T, E Q u (:554-558)
-    const int u = w.qlist[t];
-    const unsigned mask = w.pmask[u];
-    const int s = w.boff[u] + __popc(mask & ((1u << a) - 1u));
-    const double2* cp = reinterpret_cast<const double2*>(w.cb + 6 * (size_t)s);
+#pragma unroll 2
+  for (int t = q0 + lane; t < q1; t += 64) {  // E Q E^T, E Q u (:554-558)
+    const int2 qe = qlist[t];
+    const double2* cp = reinterpret_cast<const double2*>(cb + 6 * (size_t)qe.y);
     const double2 c01 = cp[0], c23 = cp[1], c45 = cp[2];
     const double c[6] = {c01.x, c01.y, c23.x, c23.y, c45.x, c45.y};
-    const double q = w.Q[u], qu = q * w.U[u];
+    const double q = Q[qe.x], qu = q * U[qe.x];
 #pragma unroll
     for (int x = 0, k = 0; x < 6; x++) {
       const double cq = c[x] * q;
@@ -578,38 +771,37 @@ __device__ void schur_diag(const BaWs& w, int a, int lane, int tau, double* Sout
       yv[x] -= c[x] * qu;
     }
   }
-  team_reduce<21>(acc, tau);
-  team_reduce<6>(yv, tau);
-  double* Sb = Sout + 36 * (size_t)blk(a, a);
+  team_reduce<21>(acc, 64);
+  team_reduce<6>(yv, 64);
 #pragma unroll
   for (int x = 0, k = 0; x < 6; x++)
 #pragma unroll
     for (int z = 0; z <= x; z++, k++)
-      if ((k % tau) == lane) {
+      if (k == lane) {
         Sb[6 * x + z] = acc[k];
         Sb[6 * z + x] = acc[k];
       }
 #pragma unroll
   for (int x = 0; x < 6; x++)
-    if (((21 + x) % tau) == lane) yout[6 * a + x] = yv[x];
+    if (21 + x == lane) ya[x] = yv[x];
 }
 
-// off-diagonal block (a, b), a > b: walks the shorter of the two pose lists
-__device__ void schur_off(const BaWs& w, int a, int b, int lane, int tau, double* Sout) {
+// off-diagonal block (a, b), a > b: exactly the pair's edge and patch ranges
+__device__ __forceinline__ void schur_off(const int32_t* __restrict__ elist,
+                                          const int2* __restrict__ qplist,
+                                          const float* __restrict__ J,
+                                          const double* __restrict__ Q,
+                                          const double* __restrict__ cb, int e0, int e1, int q0,
+                                          int q1, int lane, int tau, double* Sb) {
   double acc[36];
 #pragma unroll
   for (int i = 0; i < 36; i++) acc[i] = 0.0;
-  const int la = w.eoff[a + 1] - w.eoff[a], lb = w.eoff[b + 1] - w.eoff[b];
-  const int sp = (lb < la) ? b : a, other = (sp == a) ? b : a;
-  const int e1 = w.eoff[sp + 1];
-  for (int t = w.eoff[sp] + lane; t < e1; t += tau) {  // B_ab = -sum w Ji_a^T Jj_b
-    const int ent = w.elist[t];
-    if (((ent >> 2) & 31) != other) continue;
-    // rows of the block follow pose a: Ji when ii == a, Jj when jj == a
-    const bool rows_i = (sp == a) ? (ent & 1) : (ent & 2);
-    const float* o = w.J + (size_t)kJStride * (ent >> 8);
-    const float* orow = o + (rows_i ? 6 : 18);
-    const float* ocol = o + (rows_i ? 18 : 6);
+  for (int t = e0 + lane; t < e1; t += tau) {  // B_ab = -sum w J_a^T J_b
+    const int ent = elist[t];
+    // rows follow pose a: Ji when ii == a (roles bit 0), Jj when jj == a
+    const float* o = J + (size_t)kJStride * (ent >> 8);
+    const float* orow = o + ((ent & 1) ? 6 : 18);
+    const float* ocol = o + ((ent & 1) ? 18 : 6);
 #pragma unroll 1
     for (int row = 0; row < 2; row++) {
       const double wr = o[row];
@@ -627,23 +819,17 @@ __device__ void schur_off(const BaWs& w, int a, int b, int lane, int tau, double
       }
     }
   }
-  const int qa = w.qoff[a + 1] - w.qoff[a], qb = w.qoff[b + 1] - w.qoff[b];
-  const int qp = (qb < qa) ? b : a, qo = (qp == a) ? b : a;
-  const int q1 = w.qoff[qp + 1];
-  for (int t = w.qoff[qp] + lane; t < q1; t += tau) {
-    const int u = w.qlist[t];
-    const unsigned mask = w.pmask[u];
-    if (!((mask >> qo) & 1u)) continue;
-    const int s0 = w.boff[u];
-    const double* ca = w.cb + 6 * (size_t)(s0 + __popc(mask & ((1u << a) - 1u)));
-    const double* cc = w.cb + 6 * (size_t)(s0 + __popc(mask & ((1u << b) - 1u)));
+  for (int t = q0 + lane; t < q1; t += tau) {
+    const int2 qe = qplist[t];
+    const double* ca = cb + 6 * (size_t)(qe.y & 0xffff);
+    const double* cc = cb + 6 * (size_t)(qe.y >> 16);
     double va[6], vb[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) {
       va[k] = ca[k];
       vb[k] = cc[k];
     }
-    const double q = w.Q[u];
+    const double q = Q[qe.x];
 #pragma unroll
     for (int x = 0; x < 6; x++) {
       const double cq = va[x] * q;
@@ -652,209 +838,186 @@ __device__ void schur_off(const BaWs& w, int a, int b, int lane, int tau, double
     }
   }
   team_reduce<36>(acc, tau);
-  double* Sb = Sout + 36 * (size_t)blk(a, b);
 #pragma unroll
   for (int k = 0; k < 36; k++)
     if ((k % tau) == lane) Sb[k] = acc[k];
 }
 
-__device__ __forceinline__ int pow2_floor(int v) {
-  int p = 1;
-  while (2 * p <= v) p *= 2;
-  return p;
-}
-
 __device__ void ba_schur_phase(const BaWs& w, int N, double* Sout, double* yout) {
-  const int tid = threadIdx.x, T = blockDim.x;
-  // diagonal blocks (the heavy ones): one team of up to a wave each
-  {
-    const int tau = min(64, pow2_floor(T / N));
-    const int team = tid / tau, lane = tid % tau, nteam = T / tau;
-    for (int a = team; a < N; a += nteam) schur_diag(w, a, lane, tau, Sout, yout);
-  }
-  // off-diagonal blocks, assigned from the last team down so they land on
-  // the waves the diagonal pass left idle
-  const int noff = N * (N - 1) / 2;
-  if (noff > 0) {
-    const int tau = min(64, pow2_floor(max(1, T / noff)));
-    const int nteam = T / tau, team = nteam - 1 - tid / tau, lane = tid % tau;
-    for (int d = team; d < noff; d += nteam) {
-      const int a = 1 + tri_row(d), b = d - a * (a - 1) / 2;  // a > b
-      schur_off(w, a, b, lane, tau, Sout);
-    }
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int a = wid; a < N; a += kBaWaves)
+    schur_diag(w.elist, w.qlist, w.J, w.Q, w.U, w.cb, w.eoff[a], w.eoff[a + 1], w.qoff[a],
+               w.qoff[a + 1], lane, Sout + 36 * (size_t)blk(a, a), yout + 6 * a);
+  constexpr int tau = 16;
+  const int noff = N * (N - 1) / 2, nteam = blockDim.x / tau;
+  const int team = nteam - 1 - tid / tau, tl = tid % tau;
+  for (int d = team; d < noff; d += nteam) {
+    const int a = 1 + tri_row(d), b = d - a * (a - 1) / 2;  // a > b
+    schur_off(w.elist, w.qplist, w.J, w.Q, w.cb, w.epair[a * kPairStride + b],
+              w.epair[a * kPairStride + b + 1], w.qpair[a * kPairStride + b],
+              w.qpair[a * kPairStride + b + 1], tl, tau, Sout + 36 * (size_t)blk(a, b));
   }
 }
 
 // ---------------------------------------------------------------------------
-// SOLVE: S (lower blocks, LDS) -> L; y -> x.  L_kk^{-1} kept per block.
+// SOLVE: damped S (lower blocks, LDS) -> L in place; y -> dX in place.
+// rd[6k + c] = 1 / L_kk[c][c].
 // ---------------------------------------------------------------------------
-// one lane: in-place Cholesky of the 6x6 block (lower), its inverse to Li.
-// Packed lower storage (21 doubles each) keeps it in registers.
-__device__ __forceinline__ constexpr int lt(int r, int c) { return r * (r + 1) / 2 + c; }
+__device__ __forceinline__ double rsqrt_d(double x) {  // hardware estimate + 2 Newton steps
+  double r = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  r = r * (1.5 - h * r * r);
+  r = r * (1.5 - h * r * r);
+  return r;
+}
 
-__device__ __noinline__ void factor_diag(double* Sb, double* Li, int* fail) {
-  double L[21], inv[6];
-#pragma unroll
-  for (int r = 0; r < 6; r++)
-#pragma unroll
-    for (int c = 0; c <= r; c++) L[lt(r, c)] = Sb[6 * r + c];
+// one wave: Cholesky of the 6x6 pivot block, lane (r, c) = 6r + c holds
+// element (r, c); column steps broadcast through shuffles.
+__device__ __forceinline__ bool factor_pivot_block(double* Sb, double* rd) {
+  const int lane = threadIdx.x & 63, r6 = lane / 6, c6 = lane - 6 * (lane / 6);
+  const bool act = lane < 36;
+  double v = act ? Sb[lane] : 0.0;
   bool ok = true;
 #pragma unroll
   for (int c = 0; c < 6; c++) {
-    const double d = L[lt(c, c)];
-    ok = ok && (d > 0.0);
-    const double s = sqrt(d);
-    inv[c] = 1.0 / s;
-    L[lt(c, c)] = s;
-#pragma unroll
-    for (int r = c + 1; r < 6; r++) L[lt(r, c)] *= inv[c];
-#pragma unroll
-    for (int c2 = c + 1; c2 < 6; c2++)
-#pragma unroll
-      for (int r = c2; r < 6; r++) L[lt(r, c2)] -= L[lt(r, c)] * L[lt(c2, c)];
+    const double piv = __shfl(v, 7 * c, 64);
+    ok = ok && (piv > 0.0);
+    const double rs = rsqrt_d(piv);
+    if (act && c6 == c) v = (r6 == c) ? piv * rs : (r6 > c ? v * rs : v);
+    if (lane == c) rd[c] = rs;
+    const double lr = __shfl(v, min(6 * r6 + c, 63), 64);
+    const double lc = __shfl(v, min(6 * c6 + c, 63), 64);
+    if (act && c6 > c && r6 >= c6) v -= lr * lc;
   }
-#pragma unroll
-  for (int r = 0; r < 6; r++)
-#pragma unroll
-    for (int c = 0; c < 6; c++) Sb[6 * r + c] = c <= r ? L[lt(r, c)] : 0.0;
-  double X[21];  // X = L^{-1}, lower
-#pragma unroll
-  for (int i = 0; i < 6; i++) {
-    X[lt(i, i)] = inv[i];
-#pragma unroll
-    for (int j = 0; j < i; j++) {
-      double s = 0.0;
-#pragma unroll
-      for (int k = j; k < i; k++) s += L[lt(i, k)] * X[lt(k, j)];
-      X[lt(i, j)] = -s * inv[i];
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 6; r++)
-#pragma unroll
-    for (int c = 0; c < 6; c++) Li[6 * r + c] = (ok && c <= r) ? X[lt(r, c)] : 0.0;
-  if (!ok) *fail = 1;
+  if (act) Sb[lane] = (c6 <= r6) ? v : 0.0;
+  return ok;
 }
 
-// x = dX in y (LDS); returns through LDS.  All threads call.
-__device__ void ba_solve_phase(int N, double* S, double* Linv, double* y, int* fail) {
-  const int tid = threadIdx.x, T = blockDim.x;
-  if (tid == 0) *fail = 0;
+// row r of block (a, b) -= row r of L_ak times L_bk^T
+__device__ __forceinline__ void trailing_row(double* S, int k, int a, int b, int r) {
+  const double* la = S + 36 * (size_t)blk(a, k) + 6 * r;
+  const double* lb = S + 36 * (size_t)blk(b, k);
+  double* row = S + 36 * (size_t)blk(a, b) + 6 * r;
+  double lr[6];
+#pragma unroll
+  for (int q = 0; q < 6; q++) lr[q] = la[q];
+#pragma unroll
+  for (int c = 0; c < 6; c++) {
+    double v = row[c];
+#pragma unroll
+    for (int q = 0; q < 6; q++) v -= lr[q] * lb[6 * c + q];
+    row[c] = v;
+  }
+}
+
+__device__ void ba_solve_phase(int N, double* S, double* rd, double* y, int* fail,
+                               int64_t* tr = nullptr) {
+  const int tid = threadIdx.x, T = blockDim.x, wid = tid >> 6, lane = tid & 63;
   for (int t = tid; t < 6 * N; t += T) {  // S += I * (1e-4 S + 1)  (ba_cuda.cu:560)
     double* d = S + 36 * (size_t)blk(t / 6, t / 6) + 7 * (t % 6);
     *d += 1e-4 * *d + 1.0;
   }
   __syncthreads();
-  if (tid == 0) factor_diag(S, Linv, fail);
+  if (wid == 0) {
+    const bool ok = factor_pivot_block(S, rd);
+    if (lane == 0) *fail = ok ? 0 : 1;
+  }
   __syncthreads();
+  trace(tr, 50);
   for (int k = 0; k < N; k++) {
-    const int m = N - k - 1;  // remaining poses below k
-    const double* Lk = Linv + 36 * k;
-    // panel: L_ak = S_ak L_kk^{-T}
-    for (int t = tid; t < 6 * m; t += T) {
-      const int a = k + 1 + t / 6, r = t % 6;
-      double* row = S + 36 * (size_t)blk(a, k) + 6 * r;
-      double s[6], o[6];
+    const int m = N - k - 1;
+    // panel: L_ak = S_ak L_kk^{-T} by substitution, one row per thread
+    {
+      const double* Lkk = S + 36 * (size_t)blk(k, k);
+      const double* rk = rd + 6 * k;
+      for (int t = tid; t < 6 * m; t += T) {
+        const int a = k + 1 + t / 6, r = t % 6;
+        double* row = S + 36 * (size_t)blk(a, k) + 6 * r;
+        double x[6];
 #pragma unroll
-      for (int c = 0; c < 6; c++) s[c] = row[c];
-#pragma unroll
-      for (int c = 0; c < 6; c++) {
-        double v = 0.0;
-#pragma unroll
-        for (int q = 0; q <= c; q++) v += s[q] * Lk[6 * c + q];
-        o[c] = v;
-      }
-#pragma unroll
-      for (int c = 0; c < 6; c++) row[c] = o[c];
-    }
-    __syncthreads();
-    if (m == 0) break;
-    // trailing: S_ab -= L_ak L_bk^T for k < b <= a; wave 0 updates block
-    // (k+1, k+1) and factors it while the other waves do the rest
-    if (tid < 64) {
-      if (tid < 6) {
-        const double* la = S + 36 * (size_t)blk(k + 1, k) + 6 * tid;
-        double* row = S + 36 * (size_t)blk(k + 1, k + 1) + 6 * tid;
-        double lr[6];
-#pragma unroll
-        for (int q = 0; q < 6; q++) lr[q] = la[q];
+        for (int c = 0; c < 6; c++) x[c] = row[c];
 #pragma unroll
         for (int c = 0; c < 6; c++) {
-          const double* lc = S + 36 * (size_t)blk(k + 1, k) + 6 * c;
-          double v = row[c];
+          double s = x[c];
 #pragma unroll
-          for (int q = 0; q < 6; q++) v -= lr[q] * lc[q];
-          row[c] = v;
+          for (int q = 0; q < c; q++) s -= x[q] * Lkk[6 * c + q];
+          x[c] = s * rk[c];
         }
+#pragma unroll
+        for (int c = 0; c < 6; c++) row[c] = x[c];
       }
+    }
+    __syncthreads();
+    trace(tr, 51 + 2 * k);
+    if (m == 0) break;
+    // trailing update; wave 0 takes block (k+1, k+1) and factors it right
+    // away (look-ahead) while the other waves update the rest
+    if (wid == 0) {
+      if (lane < 6) trailing_row(S, k, k + 1, k + 1, lane);
       wave_lds_sync();
-      if (tid == 0) factor_diag(S + 36 * (size_t)blk(k + 1, k + 1), Linv + 36 * (k + 1), fail);
+      const bool ok = factor_pivot_block(S + 36 * (size_t)blk(k + 1, k + 1), rd + 6 * (k + 1));
+      if (!ok && lane == 0) *fail = 1;
     } else {
       const int ntask = 6 * (m * (m + 1) / 2 - 1);
       for (int t = tid - 64; t < ntask; t += T - 64) {
         const int j = 1 + t / 6, r = t % 6;
         const int ap = tri_row(j), bp = j - ap * (ap + 1) / 2;
-        const int a = k + 1 + ap, b = k + 1 + bp;
-        const double* la = S + 36 * (size_t)blk(a, k) + 6 * r;
-        double* row = S + 36 * (size_t)blk(a, b) + 6 * r;
-        double lr[6];
-#pragma unroll
-        for (int q = 0; q < 6; q++) lr[q] = la[q];
-#pragma unroll
-        for (int c = 0; c < 6; c++) {
-          const double* lc = S + 36 * (size_t)blk(b, k) + 6 * c;
-          double v = row[c];
-#pragma unroll
-          for (int q = 0; q < 6; q++) v -= lr[q] * lc[q];
-          row[c] = v;
-        }
+        trailing_row(S, k, k + 1 + ap, k + 1 + bp, r);
       }
     }
     __syncthreads();
+    trace(tr, 52 + 2 * k);
   }
-  __syncthreads();
   if (*fail) {
     for (int t = tid; t < 6 * N; t += T) y[t] = 0.0;  // dX = 0 (dpvo/ba.py:17-21)
-  } else if (tid < 64) {
-    // forward: z_k = L_kk^{-1} (y_k - sum_{b<k} L_kb z_b), right-looking
+  } else if (wid == 0) {
+    // forward: z_k = L_kk^{-1} y_k, then y_a -= L_ak z_k (a > k); every lane
+    // keeps z_k in registers
     for (int k = 0; k < N; k++) {
-      double z = 0.0;
-      if (tid < 6) {
-        const double* Lk = Linv + 36 * k + 6 * tid;
+      const double* Lkk = S + 36 * (size_t)blk(k, k);
+      double z[6];
 #pragma unroll
-        for (int c = 0; c < 6; c++) z += Lk[c] * y[6 * k + c];
+      for (int r = 0; r < 6; r++) {
+        double s = y[6 * k + r];
+#pragma unroll
+        for (int q = 0; q < r; q++) s -= Lkk[6 * r + q] * z[q];
+        z[r] = s * rd[6 * k + r];
       }
-      wave_lds_sync();
-      if (tid < 6) y[6 * k + tid] = z;
-      wave_lds_sync();
-      for (int t = tid; t < 6 * (N - k - 1); t += 64) {
+      for (int t = lane; t < 6 * (N - k - 1); t += 64) {
         const int a = k + 1 + t / 6, r = t % 6;
         const double* la = S + 36 * (size_t)blk(a, k) + 6 * r;
         double v = y[6 * a + r];
 #pragma unroll
-        for (int c = 0; c < 6; c++) v -= la[c] * y[6 * k + c];
+        for (int c = 0; c < 6; c++) v -= la[c] * z[c];
         y[6 * a + r] = v;
       }
+#pragma unroll
+      for (int r = 0; r < 6; r++)
+        if (lane == r) y[6 * k + r] = z[r];
       wave_lds_sync();
     }
-    // backward: x_k = L_kk^{-T} (z_k - sum_{a>k} L_ak^T x_a)
+    // backward: x_k = L_kk^{-T} z_k, then z_b -= L_kb^T x_k (b < k)
     for (int k = N - 1; k >= 0; k--) {
-      double x = 0.0;
-      if (tid < 6) {
+      const double* Lkk = S + 36 * (size_t)blk(k, k);
+      double x[6];
 #pragma unroll
-        for (int c = 0; c < 6; c++) x += Linv[36 * k + 6 * c + tid] * y[6 * k + c];
+      for (int r = 5; r >= 0; r--) {
+        double s = y[6 * k + r];
+#pragma unroll
+        for (int q = r + 1; q < 6; q++) s -= Lkk[6 * q + r] * x[q];
+        x[r] = s * rd[6 * k + r];
       }
-      wave_lds_sync();
-      if (tid < 6) y[6 * k + tid] = x;
-      wave_lds_sync();
-      for (int t = tid; t < 6 * k; t += 64) {
+      for (int t = lane; t < 6 * k; t += 64) {
         const int b = t / 6, r = t % 6;
         const double* lk = S + 36 * (size_t)blk(k, b);
         double v = y[6 * b + r];
 #pragma unroll
-        for (int c = 0; c < 6; c++) v -= lk[6 * c + r] * y[6 * k + c];
+        for (int c = 0; c < 6; c++) v -= lk[6 * c + r] * x[c];
         y[6 * b + r] = v;
       }
+#pragma unroll
+      for (int r = 0; r < 6; r++)
+        if (lane == r) y[6 * k + r] = x[r];
       wave_lds_sync();
     }
   }
@@ -864,6 +1027,36 @@ __device__ void ba_solve_phase(int N, double* S, double* Linv, double* y, int* f
 // ---------------------------------------------------------------------------
 // UPDATE: pose_retr_kernel (:178-206), dZ (:563), patch_retr_kernel (:209-229)
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void patch_retract(const int32_t* __restrict__ boff,
+                                              const int32_t* __restrict__ bpose,
+                                              const double* __restrict__ cb,
+                                              const double* __restrict__ Q,
+                                              const double* __restrict__ U,
+                                              const int64_t* __restrict__ kx, const double* x,
+                                              int nuniq, int P, float* __restrict__ patches) {
+  for (int u = threadIdx.x; u < nuniq; u += blockDim.x) {
+    double s = U[u];
+    for (int b = boff[u]; b < boff[u + 1]; b++) {
+      const int p = bpose[b];
+      const double2* c = reinterpret_cast<const double2*>(cb + 6 * (size_t)b);
+      const double2 c01 = c[0], c23 = c[1], c45 = c[2];
+      const double* xp = x + 6 * p;
+      s -= c01.x * xp[0];
+      s -= c01.y * xp[1];
+      s -= c23.x * xp[2];
+      s -= c23.y * xp[3];
+      s -= c45.x * xp[4];
+      s -= c45.y * xp[5];
+    }
+    const float dz = (float)(Q[u] * s);
+    float* pk = patches + (size_t)kx[u] * 3 * P * P + 2 * P * P;
+    float d = pk[0] + dz;
+    d = (d > 20.0f) ? 1.0f : d;
+    d = (float)fmax((double)d, 1e-4);
+    for (int k = 0; k < P * P; k++) pk[k] = d;
+  }
+}
+
 __device__ void ba_update_phase(const BaArgs& A, const BaWs& w, const double* x, int fail,
                                 double* dX_out) {
   const int tid = threadIdx.x, T = blockDim.x, N = A.N;
@@ -884,50 +1077,36 @@ __device__ void ba_update_phase(const BaArgs& A, const BaWs& w, const double* x,
     pt[0] = t1[0]; pt[1] = t1[1]; pt[2] = t1[2];
     pt[3] = q1[0]; pt[4] = q1[1]; pt[5] = q1[2]; pt[6] = q1[3];
   }
-  const int nuniq = w.meta[0], P = A.P;
-  for (int u = tid; u < nuniq; u += T) {
-    double s = w.U[u];
-    for (int b = w.boff[u]; b < w.boff[u + 1]; b++) {
-      const int p = w.bpose[b];
-      const double* c = w.cb + 6 * (size_t)b;
-#pragma unroll
-      for (int k = 0; k < 6; k++) s -= c[k] * x[6 * p + k];
-    }
-    const float dz = (float)(w.Q[u] * s);
-    float* pk = A.patches + (size_t)w.kx[u] * 3 * P * P + 2 * P * P;
-    float d = pk[0] + dz;
-    d = (d > 20.0f) ? 1.0f : d;
-    d = (float)fmax((double)d, 1e-4);
-    for (int k = 0; k < P * P; k++) pk[k] = d;
-  }
+  patch_retract(w.boff, w.bpose, w.cb, w.Q, w.U, w.kx, x, w.meta[0], A.P, A.patches);
 }
 
 // LDS carve of the solve region
 struct SolveLds {
   int* ctl;
   double* S;
-  double* Linv;
+  double* rd;
   double* y;
 };
 __device__ __forceinline__ SolveLds solve_carve(char* lds, int N) {
   SolveLds s;
   s.ctl = reinterpret_cast<int*>(lds);
   s.S = reinterpret_cast<double*>(lds + kCtlBytes);
-  s.Linv = s.S + 36 * (N * (N + 1) / 2);
-  s.y = s.Linv + 36 * N;
+  s.rd = s.S + 36 * (N * (N + 1) / 2);
+  s.y = s.rd + 6 * N;
   return s;
 }
 
 // one BA call: setup + all iterations in one workgroup.  Thread 0 stamps
 // the 100 MHz wall clock after every phase (dpvo_ba_phase_marks).
 __device__ __forceinline__ void mark(const BaWs& w, int slot) {
-  if (threadIdx.x == 0 && slot < kMarks) w.tmark[slot] = (int64_t)wall_clock64();
+  if (threadIdx.x == 0 && slot < 38) w.tmark[slot] = (int64_t)wall_clock64();
 }
 
 __global__ void __launch_bounds__(kBaThreads)
     ba_fused_kernel(BaArgs A, BaWs w, int P2, int iterations) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   mark(w, 0);
+  if (threadIdx.x == 0) w.tmark[38] = (int64_t)clock64();
   ba_setup_phase(A, w, lds, P2);
   mark(w, 1);
   const SolveLds L = solve_carve(lds, A.N);
@@ -944,7 +1123,7 @@ __global__ void __launch_bounds__(kBaThreads)
       ba_schur_phase(w, A.N, L.S, L.y);
       __syncthreads();
       mark(w, m0 + 2);
-      ba_solve_phase(A.N, L.S, L.Linv, L.y, L.ctl + 1);
+      ba_solve_phase(A.N, L.S, L.rd, L.y, L.ctl + 1, it == 0 ? w.tmark : nullptr);
       fail = L.ctl[1];
     }
     mark(w, m0 + 3);
@@ -952,6 +1131,7 @@ __global__ void __launch_bounds__(kBaThreads)
     __syncthreads();
     mark(w, m0 + 4);
   }
+  if (threadIdx.x == 0) w.tmark[39] = (int64_t)clock64();
 }
 
 __global__ void __launch_bounds__(kBaThreads) ba_setup_kernel(BaArgs A, BaWs w, int P2) {
@@ -978,7 +1158,7 @@ __global__ void __launch_bounds__(kBaThreads)
     for (int t = threadIdx.x; t < 36 * NL; t += blockDim.x) L.S[t] = S_in[t];
     for (int t = threadIdx.x; t < 6 * N; t += blockDim.x) L.y[t] = y_in[t];
     __syncthreads();
-    ba_solve_phase(N, L.S, L.Linv, L.y, L.ctl + 1);
+    ba_solve_phase(N, L.S, L.rd, L.y, L.ctl + 1);
     fail = L.ctl[1];
   }
   ba_update_phase(A, w, L.y, fail, dX_out);

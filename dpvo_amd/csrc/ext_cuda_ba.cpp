@@ -68,7 +68,7 @@ std::vector<torch::Tensor> ba_forward(torch::Tensor poses, torch::Tensor patches
   return {};
 }
 
-// Same call; returns the fused kernel's 32 wall-clock marks (100 MHz ticks:
+// Same call; returns the fused kernel's 256 wall-clock marks (100 MHz ticks:
 // start, setup, then linearize/patch/schur/solve/update per iteration).
 torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
                                torch::Tensor intrinsics, torch::Tensor target, torch::Tensor weight,
@@ -77,7 +77,7 @@ torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
                                bool eff_impl) {
   auto ws = ba_forward_ws(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, PPF, t0,
                           t1, iterations, eff_impl);
-  auto out = torch::zeros({32}, poses.options().dtype(torch::kInt64));
+  auto out = torch::zeros({256}, poses.options().dtype(torch::kInt64));
   if (!ws.defined()) return out;
   check_status(dpvo_ba_phase_marks(ws.data_ptr(), ii.numel(), t0, t1, out.data_ptr<int64_t>(),
                                    current_stream()),

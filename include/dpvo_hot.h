@@ -135,10 +135,11 @@ int dpvo_ba_solve_update(float* poses, float* patches, const double* S_lower, co
    `out`: bit 0 = Cholesky failed in the last solve (dX was set to 0),
    bit 1 = some kk outside [0, num_patches) (clamped). */
 int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1, int* out, void* stream);
-/* Instrumentation (no reference counterpart): the 32 wall-clock marks
-   (100 MHz) the last dpvo_ba_forward on this workspace stamped after each
-   phase -- [0] start, [1] setup, then linearize, patch, schur, solve, update
-   per iteration -- copied to the DEVICE array `out`. */
+/* Instrumentation (no reference counterpart): the 256 marks the last
+   dpvo_ba_forward on this workspace stamped -- wall clock (100 MHz): [0]
+   start, [1] setup, then linearize, patch, schur, solve, update per iteration;
+   shader clock: [38] start, [39] end; [40..] finer stamps inside the setup
+   and the first solve -- copied to the DEVICE array `out`. */
 int dpvo_ba_phase_marks(const void* workspace, int E, int t0, int t1, int64_t* out, void* stream);
 
 /* F-REPROJ.  Replaces cuda_ba.reproject (ba.cpp:47-53 -> cuda_reproject,

@@ -1,5 +1,8 @@
-"""Per-phase timing of the fused F-BA kernel on cfg2 (GPU): wall-clock marks
-stamped by thread 0 after every phase (cuda_ba.forward_marks)."""
+"""Per-phase timing of the fused F-BA kernel (GPU): wall-clock marks stamped
+by thread 0 after every phase (cuda_ba.forward_marks), medians over reps.
+
+    python scripts/ba_phases.py [cfg] [iterations]
+"""
 import os
 import sys
 
@@ -15,25 +18,43 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 G = synthetic.make_config(cfg, seed=0)
 D = G.to(dev)
+N = G.F - 1
 lm = torch.tensor([1e-4], device=dev)
 names = ["linearize", "patch", "schur", "solve", "update"]
 acc = {}
-for rep in range(20):
+for rep in range(25):
     poses, patches = D.poses.clone(), D.patches.clone()
     m = cb.forward_marks(poses, patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj, D.kk,
                          G.M, 1, G.F, iters, False).cpu().tolist()
     if rep < 5:
         continue
-    d = {"setup": m[1] - m[0]}
-    prev = m[1]
+    d = {}
+    prev = m[0]
+    for k, slot in [("sort", 40), ("ranks", 41), ("masks+slots", 42), ("elists", 43),
+                    ("qlists", 44), ("epart", 45), ("qpart", 1)]:
+        d["setup." + k] = m[slot] - prev
+        prev = m[slot]
     for it in range(iters):
         for k, n in enumerate(names):
             t = m[2 + 5 * it + k]
+            if it == 0 and n == "solve":  # fine stamps of the first solve
+                p2 = m[4]
+                d["solve.factor0"] = m[50] - p2
+                p2 = m[50]
+                for kk in range(N):
+                    d[f"solve.panel{kk}"] = m[51 + 2 * kk] - p2
+                    p2 = m[51 + 2 * kk]
+                    if kk < N - 1:
+                        d[f"solve.trail{kk}"] = m[52 + 2 * kk] - p2
+                        p2 = m[52 + 2 * kk]
+                d["solve.subst"] = t - p2
             d[f"{n}{it}"] = t - prev
             prev = t
     d["total"] = prev - m[0]
     for k, v in d.items():
         acc.setdefault(k, []).append(v * 10.0 / 1000.0)  # 100 MHz ticks -> us
+    # shader clock cycles / wall time: the core clock the kernel ran at
+    acc.setdefault("clock_MHz", []).append((m[39] - m[38]) / max(1, prev - m[0]) * 100.0)
 for k, v in acc.items():
     v.sort()
-    print(f"{k:12s} median {v[len(v) // 2]:8.2f} us")
+    print(f"{k:16s} median {v[len(v) // 2]:8.2f}", "MHz" if k == "clock_MHz" else "us")
