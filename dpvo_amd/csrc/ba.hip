@@ -6,76 +6,63 @@
 //   Q = 1/(C+lmbda); S = B - E Q E^T; y = v - E Q u; S += I*(1e-4 S + 1)
 //   dX = chol_solve(S, y); dZ = Q (u - E^T dX); pose / patch retraction.
 //
-// MI355X design (DESIGN.md "F-BA").  A DPVO window is small (N <= 20 free
-// poses, a few thousand edges): the reference spends its time in ~15 kernel
-// launches, float atomics and a host-side Cholesky per iteration.  Here a BA
-// call -- setup and every iteration -- is ONE workgroup of 1024 threads,
-// phases separated by barriers, no float atomics, every reduction in a fixed
-// order (bitwise deterministic).  On one CU the enemy is the chain of
-// DEPENDENT global loads (~1 us each under load), so the setup pays once to
-// make every later phase one or two loads deep:
-//   setup      sort (kk, edge) in LDS (bitonic) -> "sorted positions": edges
-//              grouped by patch.  Per position a record (edge, ii, jj, kk)
-//              and the pose-block slots of its two poses; per patch the free
-//              pose mask and block offsets; per pose the edge list and the
-//              patch list, each partitioned (wave ballots, stable) into exact
-//              per-pose-pair ranges for the off-diagonal Schur blocks.
-//   linearize  thread per position: the fp32 edge math of the reference
-//              -> J (fp32) and the edge's E/C/u terms (fp64), position order.
-//   patch      thread per patch: Q_u, U_u and the E column blocks c_{u,p}.
-//   schur      gather, one wave per diagonal block, 16-lane teams per
-//              off-diagonal block, each walking exactly its list range;
-//              S (lower 6x6 blocks) and y land in LDS.
-//   solve      damping; one wave: right-looking block Cholesky in LDS, the
-//              6x6 pivot blocks factored across 36 lanes (rsq + Newton),
-//              panels by substitution; block forward/back substitution.
-//   update     pose retraction, dZ = Q (u - E^T dX), patch retraction.
-// The split (build_schur -> all-reduce(S,y) -> solve_update) runs the same
-// phases in three single-workgroup kernels: the edge-sharded multi-GPU form
-// (SURVEY 8e).
+// MI355X design (DESIGN.md "F-BA"), shaped by measured gfx950 costs
+// (scripts/micro): barrier ~70 ns, dependent LDS load ~27 ns, dependent L2
+// load ~60-175 ns, dependent fp64 FMA 36 cycles, back-to-back launch 2.4 us.
+// A DPVO window is tiny (N <= 20 free poses, a few thousand edges), so one
+// CU runs out of latency hiding long before it runs out of FLOPs; the work
+// is spread over ~70 CUs and the launches are kept to 1 + iterations:
+//
+//   ba_setup_kernel (1 workgroup, once per call): counting sort of the
+//       edges by patch in LDS (bitonic fallback for wide kk ranges) ->
+//       "positions" grouped by patch (edge, ii, jj, kk records), unique
+//       patches, per-patch free-pose masks and pose-block offsets.
+//   ba_iter_kernel (one launch per iteration, NL + ceil(E/512) workgroups):
+//     * one workgroup per lower 6x6 block (a, b) of S: every patch whose
+//       mask holds a and b is re-linearised by one thread (the fp32 edge
+//       math of the reference), which accumulates that patch's B, E Q E^T
+//       (and y) terms in fp64 registers; a fixed DPP tree + ordered
+//       cross-wave sum -> deterministic S block, no atomics;
+//     * patch-owner workgroups: Q_u, U_u and the E column blocks c_{u,p}
+//       of every patch (needed for dZ);
+//     * the last workgroup to arrive (one atomic ticket, agent-scope
+//       fences) damps S, runs the block Cholesky in LDS, the substitutions,
+//       the pose retraction and dZ + patch retraction.
+//   The split (build_schur -> all-reduce(S,y) -> solve_update) launches the
+//   same code without / as the solve tail: the edge-sharded multi-GPU form
+//   (SURVEY 8e).
 #include "common.hpp"
 
 namespace dpvo {
 
-constexpr int kBaThreads = 1024;
-constexpr int kBaWaves = kBaThreads / 64;
-constexpr int kMaxSetupE = 16384;  // LDS: 16384 x 8 B sort keys = 128 KiB
-constexpr int kMaxFree = 20;       // lower blocks of S for N=20: 59 KiB of LDS
-constexpr int kPerThread = kMaxSetupE / kBaThreads;
-constexpr int kJStride = 32;       // floats per edge: w[2] r[2] Jz[2] Ji[2][6] Jj[2][6]
-constexpr int kEStride = 14;       // doubles per edge: Ei[6] Ej[6] C u
-constexpr int kCtlBytes = 512;     // LDS control words + scan scratch
-constexpr int kNoPose = 31;        // "other pose" code of an edge with one free end
-constexpr int kMarks = 256;        // [0..37] phases, [38..39] clock, [40..] detailed trace
-constexpr int kPairStride = 32;    // row stride of the pair-offset tables
+constexpr int kSetupThreads = 1024;
+constexpr int kIterThreads = 512;
+constexpr int kIterWaves = kIterThreads / 64;
+constexpr int kMaxSetupE = 16384;
+constexpr int kMaxFree = 20;  // pose-block masks are 32-bit; lower S blocks of N=20: 59 KiB LDS
+constexpr int kPerThread = kMaxSetupE / kSetupThreads;
+constexpr int kCtlBytes = 512;
+constexpr int kSetupLds = 160 * 1024;
+constexpr int kMarks = 64;
+constexpr int kNoPose = 31;
+constexpr int kRegBlocks = 4;
 
 struct BaWs {
-  int4* srec;       // [E]   per sorted position: edge id, ii, jj (clamped), kk (clamped)
-  int32_t* eslot;   // [E]   per position: block slot of ii | slot of jj << 8 (0xff = fixed)
-  int32_t* poff;    // [E+1] patch -> position range
+  int4* srec;       // [E]   per position: edge id, ii, jj, kk (clamped to the patch buffer)
+  int32_t* poff;    // [E+1] patch -> position range (positions grouped by patch, edges ascending)
   int32_t* boff;    // [E+1] patch -> pose-block range
   int32_t* bpose;   // [2E]  free pose of each block (ascending per patch)
   uint32_t* pmask;  // [E]   free poses touched by each patch
-  int32_t* eoff;    // [kMaxFree+1] pose -> range of elist
-  int32_t* elist0;  // [2E]  scratch: per pose, position order
-  int32_t* elist;   // [2E]  per pose: (position << 8) | (other pose << 2) | roles,
-                    //       stable-partitioned: other = 0..a-1 first (pair ranges)
-  int32_t* epair;   // [kMaxFree][32] start of pair (a, b) in elist, b <= a ([a] = end)
-  int32_t* qoff;    // [kMaxFree+1] pose -> range of qlist
-  int2* qlist;      // [2E]  per pose: (patch, its block index for this pose)
-  int32_t* qpair;   // [kMaxFree][32] start of pair (a, b) in qplist, b <= a ([a] = end)
-  int2* qplist;     // [E*(kMaxFree-1)] patches in a and b: (patch, blk_a | blk_b << 16)
-  int32_t* meta;    // [8]   nuniq, status, nblocks, num_patches
+  int32_t* meta;    // [8]   nuniq, status, nblocks, num_patches, arrival ticket
   int64_t* kx;      // [E]   unique patch ids (ascending)
-  float* J;         // [E][32]   by position
-  double* EC;       // [E][14]   by position
   double* Q;        // [E]
   double* U;        // [E]
   double* cb;       // [2E][6]
-  double* S;        // [NL][36] (split API default)
+  double* S;        // [NL][36]
   double* y;        // [6N]
   double* dX;       // [6N]
   int64_t* tmark;   // [kMarks]
+  int64_t* wgt;     // [2 x grid] per-workgroup start / end stamps of the last iteration launch
 };
 
 struct BaArgs {
@@ -95,7 +82,6 @@ static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; 
 
 static size_t ba_layout(int E, int N, char* base, BaWs* w) {
   const size_t NL = (size_t)N * (N + 1) / 2;
-  const size_t npair = (size_t)E * (kMaxFree - 1);
   size_t off = 0;
   auto take = [&](size_t bytes) -> char* {
     char* p = base ? base + off : nullptr;
@@ -104,23 +90,12 @@ static size_t ba_layout(int E, int N, char* base, BaWs* w) {
   };
   BaWs t;
   t.srec = (int4*)take(sizeof(int4) * E);
-  t.eslot = (int32_t*)take(sizeof(int32_t) * E);
   t.poff = (int32_t*)take(sizeof(int32_t) * (E + 1));
   t.boff = (int32_t*)take(sizeof(int32_t) * (E + 1));
   t.bpose = (int32_t*)take(sizeof(int32_t) * 2 * E);
   t.pmask = (uint32_t*)take(sizeof(uint32_t) * E);
-  t.eoff = (int32_t*)take(sizeof(int32_t) * (kMaxFree + 1));
-  t.elist0 = (int32_t*)take(sizeof(int32_t) * 2 * E);
-  t.elist = (int32_t*)take(sizeof(int32_t) * 2 * E);
-  t.epair = (int32_t*)take(sizeof(int32_t) * kMaxFree * kPairStride);
-  t.qoff = (int32_t*)take(sizeof(int32_t) * (kMaxFree + 1));
-  t.qlist = (int2*)take(sizeof(int2) * 2 * E);
-  t.qpair = (int32_t*)take(sizeof(int32_t) * kMaxFree * kPairStride);
-  t.qplist = (int2*)take(sizeof(int2) * npair);
   t.meta = (int32_t*)take(sizeof(int32_t) * 8);
   t.kx = (int64_t*)take(sizeof(int64_t) * E);
-  t.J = (float*)take(sizeof(float) * kJStride * E);
-  t.EC = (double*)take(sizeof(double) * kEStride * E);
   t.Q = (double*)take(sizeof(double) * E);
   t.U = (double*)take(sizeof(double) * E);
   t.cb = (double*)take(sizeof(double) * 12 * E);
@@ -128,20 +103,15 @@ static size_t ba_layout(int E, int N, char* base, BaWs* w) {
   t.y = (double*)take(sizeof(double) * 6 * (N ? N : 1));
   t.dX = (double*)take(sizeof(double) * 6 * (N ? N : 1));
   t.tmark = (int64_t*)take(sizeof(int64_t) * kMarks);
+  t.wgt = (int64_t*)take(sizeof(int64_t) * 2 * (NL + (size_t)E / 256 + 8));
   if (w) *w = t;
   return off;
 }
 
-// LDS of the setup: [ctl][keys 8*P2] aliased after the sort by
-// [pij: 4*P2][work: 4*max(P2, N*T)]
-static size_t setup_lds(int P2, int N) {
-  const size_t work = (size_t)(P2 > N * kBaThreads ? P2 : N * kBaThreads);
-  const size_t a = 8 * (size_t)P2, b = 4 * (size_t)P2 + 4 * work;
-  return kCtlBytes + (a > b ? a : b);
-}
-static size_t solve_lds(int N) {
+// LDS of the iteration kernel: ctl | S lower blocks | rd | y | wave partials
+static size_t iter_lds(int N) {
   const size_t NL = (size_t)N * (N + 1) / 2;
-  return kCtlBytes + sizeof(double) * (36 * NL + 6 * (size_t)N + 6 * (size_t)N);
+  return kCtlBytes + sizeof(double) * (36 * NL + 12 * (size_t)N + 42 * kIterWaves);
 }
 
 __device__ __forceinline__ int tri_row(int t) {  // a with a(a+1)/2 <= t < (a+1)(a+2)/2
@@ -151,12 +121,7 @@ __device__ __forceinline__ int tri_row(int t) {  // a with a(a+1)/2 <= t < (a+1)
   return r;
 }
 __device__ __forceinline__ int blk(int a, int b) { return a * (a + 1) / 2 + b; }  // a >= b
-__device__ __forceinline__ bool is_free(int64_t p, int N) { return p >= 0 && p < N; }
-__device__ __forceinline__ unsigned long long lanemask_lt(int lane) {
-  return (1ull << lane) - 1ull;
-}
 
-// wall-clock trace stamp by thread 0 (slot < kMarks; tmark may be null)
 __device__ __forceinline__ void trace(int64_t* tmark, int slot) {
   if (tmark && threadIdx.x == 0 && slot < kMarks) tmark[slot] = (int64_t)wall_clock64();
 }
@@ -201,110 +166,196 @@ __device__ int block_exclusive_scan(int* data, int n, int* scratch) {
   return total;
 }
 
-// exclusive scan over the 64 lanes of a wave
-__device__ __forceinline__ int wave_exclusive_scan(int v, int lane) {
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(x, o, 64);
-    if (lane >= o) x += t;
-  }
-  return x - v;
-}
-
 // ---------------------------------------------------------------------------
 // SETUP: unique/inverse of kk (torch::_unique(kk, sorted, inverse),
-// ba_cuda.cu:447) and the sparse structure every later phase walks.
+// ba_cuda.cu:447) -> positions grouped by patch, masks, pose blocks.
 // ---------------------------------------------------------------------------
-__device__ void ba_setup_phase(const BaArgs& A, const BaWs& w, char* lds, int P2) {
+__global__ void __launch_bounds__(kSetupThreads) ba_setup_kernel(BaArgs A, BaWs w, int P2) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wid = tid >> 6;
   const int E = A.E, N = A.N, t0 = A.t0;
-  int* ctl = reinterpret_cast<int*>(lds);  // [0] bad kk
+  int* ctl = reinterpret_cast<int*>(lds);  // [0] bad kk [1] kmin [2] kmax
   int* scr = ctl + 64;                     // scan scratch (T/64 + 1)
-  unsigned long long* keys = reinterpret_cast<unsigned long long*>(lds + kCtlBytes);
-  int* pij = reinterpret_cast<int*>(lds + kCtlBytes);         // after the sort
-  int* work = reinterpret_cast<int*>(lds + kCtlBytes) + P2;   // after the sort
-  if (tid == 0) ctl[0] = 0;
-  __syncthreads();
-  for (int i = tid; i < P2; i += T) {
-    unsigned long long k = ~0ull;
-    if (i < E) {
-      int64_t v = A.kk[i];
-      if (v < 0 || v >= A.num_patches) {
-        ctl[0] = 1;
-        v = v < 0 ? 0 : A.num_patches - 1;
-      }
-      k = ((unsigned long long)v << 32) | (unsigned)i;
-    }
-    keys[i] = k;
-  }
-  __syncthreads();
-  for (int size = 2; size <= P2; size <<= 1) {  // bitonic sort, ascending
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < P2 / 2; i += T) {
-        const int lo = 2 * i - (i & (stride - 1));
-        const int hi = lo + stride;
-        const bool up = ((lo & size) == 0);
-        const unsigned long long a = keys[lo], b = keys[hi];
-        if ((a > b) == up) {
-          keys[lo] = b;
-          keys[hi] = a;
-        }
-      }
-      __syncthreads();
-    }
-  }
+  int* red = ctl + 96;                     // per-wave min/max (2 x 16)
+  char* mainp = lds + kCtlBytes;
+  const int budget = (kSetupLds - kCtlBytes) / 4;  // ints
   trace(w.tmark, 40);
-  // sorted position i: edge pe, patch id kv, head-of-run flag hd (registers
-  // while the key region is reused)
-  int pe[kPerThread], kv[kPerThread], hd[kPerThread];
-#pragma unroll
-  for (int k = 0; k < kPerThread; k++) {
-    const int i = tid + k * T;
-    pe[k] = kv[k] = hd[k] = 0;
-    if (i < E) {
-      const unsigned long long v = keys[i];
-      pe[k] = (int)(v & 0xffffffffu);
-      kv[k] = (int)(v >> 32);
-      hd[k] = (i == 0 || (int)(keys[i - 1] >> 32) != kv[k]) ? 1 : 0;
+  // kk range (clamped to the patch buffer; out-of-range ids flag bit 1)
+  int lmin = 0x7fffffff, lmax = -1, bad = 0;
+  for (int i = tid; i < E; i += T) {
+    int64_t v = A.kk[i];
+    if (v < 0 || v >= A.num_patches) {
+      bad = 1;
+      v = v < 0 ? 0 : A.num_patches - 1;
     }
+    lmin = min(lmin, (int)v);
+    lmax = max(lmax, (int)v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lmin = min(lmin, __shfl_xor(lmin, o, 64));
+    lmax = max(lmax, __shfl_xor(lmax, o, 64));
+    bad |= __shfl_xor(bad, o, 64);
+  }
+  if (lane == 0) {
+    red[wid] = lmin;
+    red[16 + wid] = lmax;
+    red[32 + wid] = bad;
   }
   __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kPerThread; k++) {
-    const int i = tid + k * T;
-    if (i < E) {
-      const int e = pe[k];
+  if (tid == 0) {
+    int a = 0x7fffffff, b = -1, c = 0;
+    for (int k = 0; k < T / 64; k++) {
+      a = min(a, red[k]);
+      b = max(b, red[16 + k]);
+      c |= red[32 + k];
+    }
+    ctl[0] = c;
+    ctl[1] = a;
+    ctl[2] = b;
+  }
+  __syncthreads();
+  const int kmin = ctl[1], R = ctl[2] - ctl[1] + 1;
+  const int kmaxc = A.num_patches - 1;
+  int* pij;   // per position: free-pose code of ii | of jj << 8
+  int* work;  // scratch ints (>= E)
+  int nuniq;
+  if (R + 3 * E <= budget) {
+    // ---- counting sort: histogram, packed scan (start | rank << 16),
+    // ticket placement, then each (small) bucket sorted by edge id
+    int* hist = reinterpret_cast<int*>(mainp);
+    int* spos = hist + R;
+    pij = spos + E;
+    work = pij + E;
+    for (int v = tid; v < R; v += T) hist[v] = 0;
+    __syncthreads();
+    for (int i = tid; i < E; i += T) {
+      const int v = (int)min(max(A.kk[i], (int64_t)0), (int64_t)kmaxc) - kmin;
+      atomicAdd(&hist[v], 1);
+    }
+    __syncthreads();
+    for (int v = tid; v < R; v += T) {
+      const int c = hist[v];
+      hist[v] = c | (c > 0 ? (1 << 16) : 0);
+    }
+    __syncthreads();
+    const int tot = block_exclusive_scan(hist, R, scr);
+    nuniq = tot >> 16;
+    for (int v = tid; v < R; v += T) {
+      const int h = hist[v];
+      const int nxt = (v + 1 < R) ? hist[v + 1] : tot;
+      if ((nxt >> 16) > (h >> 16)) {  // bucket v is not empty
+        w.poff[h >> 16] = h & 0xffff;
+        w.kx[h >> 16] = kmin + v;
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < E; i += T) {
+      const int v = (int)min(max(A.kk[i], (int64_t)0), (int64_t)kmaxc) - kmin;
+      spos[atomicAdd(&hist[v], 1) & 0xffff] = i;
+    }
+    if (tid == 0) w.poff[nuniq] = E;
+    __syncthreads();
+    for (int u = tid; u < nuniq; u += T) {  // insertion sort: edges ascending
+      const int a = w.poff[u], b = w.poff[u + 1];
+      for (int t = a + 1; t < b; t++) {
+        const int x = spos[t];
+        int s = t - 1;
+        while (s >= a && spos[s] > x) {
+          spos[s + 1] = spos[s];
+          s--;
+        }
+        spos[s + 1] = x;
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < E; i += T) {
+      const int e = spos[i];
       const int64_t gi = A.ii[e], gj = A.jj[e];
       const int64_t pi = gi - t0, pj = gj - t0;
-      const int ci = is_free(pi, N) ? (int)pi : kNoPose, cj = is_free(pj, N) ? (int)pj : kNoPose;
+      const int ci = (pi >= 0 && pi < N) ? (int)pi : kNoPose;
+      const int cj = (pj >= 0 && pj < N) ? (int)pj : kNoPose;
       pij[i] = ci | (cj << 8);
-      work[i] = hd[k];
-      const int ix = (int)min(max(gi, (int64_t)0), (int64_t)A.num_poses - 1);
-      const int jx = (int)min(max(gj, (int64_t)0), (int64_t)A.num_poses - 1);
-      w.srec[i] = make_int4(e, ix, jx, kv[k]);
+      const int kv = (int)min(max(A.kk[e], (int64_t)0), (int64_t)kmaxc);
+      w.srec[i] = make_int4(e, (int)gi, (int)gj, kv);
     }
-  }
-  __syncthreads();
-  const int nuniq = block_exclusive_scan(work, E, scr);
+  } else {
+    // ---- bitonic sort of (kk << 32 | edge) keys, P2 <= 16384
+    unsigned long long* keys = reinterpret_cast<unsigned long long*>(mainp);
+    for (int i = tid; i < P2; i += T) {
+      unsigned long long k = ~0ull;
+      if (i < E) {
+        const int64_t v = min(max(A.kk[i], (int64_t)0), (int64_t)kmaxc);
+        k = ((unsigned long long)v << 32) | (unsigned)i;
+      }
+      keys[i] = k;
+    }
+    __syncthreads();
+    for (int size = 2; size <= P2; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = tid; i < P2 / 2; i += T) {
+          const int lo = 2 * i - (i & (stride - 1));
+          const int hi = lo + stride;
+          const bool up = ((lo & size) == 0);
+          const unsigned long long a = keys[lo], b = keys[hi];
+          if ((a > b) == up) {
+            keys[lo] = b;
+            keys[hi] = a;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    int pe[kPerThread], kv[kPerThread], hd[kPerThread];
 #pragma unroll
-  for (int k = 0; k < kPerThread; k++) {
-    const int i = tid + k * T;
-    if (i < E && hd[k]) {
-      const int r = work[i];
-      w.kx[r] = kv[k];
-      w.poff[r] = i;
+    for (int k = 0; k < kPerThread; k++) {
+      const int i = tid + k * T;
+      pe[k] = kv[k] = hd[k] = 0;
+      if (i < E) {
+        const unsigned long long v = keys[i];
+        pe[k] = (int)(v & 0xffffffffu);
+        kv[k] = (int)(v >> 32);
+        hd[k] = (i == 0 || (int)(keys[i - 1] >> 32) != kv[k]) ? 1 : 0;
+      }
     }
+    __syncthreads();
+    pij = reinterpret_cast<int*>(mainp);
+    work = pij + E;
+#pragma unroll
+    for (int k = 0; k < kPerThread; k++) {
+      const int i = tid + k * T;
+      if (i < E) {
+        const int e = pe[k];
+        const int64_t gi = A.ii[e], gj = A.jj[e];
+        const int64_t pi = gi - t0, pj = gj - t0;
+        const int ci = (pi >= 0 && pi < N) ? (int)pi : kNoPose;
+        const int cj = (pj >= 0 && pj < N) ? (int)pj : kNoPose;
+        pij[i] = ci | (cj << 8);
+        work[i] = hd[k];
+        w.srec[i] = make_int4(e, (int)gi, (int)gj, kv[k]);
+      }
+    }
+    __syncthreads();
+    nuniq = block_exclusive_scan(work, E, scr);
+#pragma unroll
+    for (int k = 0; k < kPerThread; k++) {
+      const int i = tid + k * T;
+      if (i < E && hd[k]) {
+        w.kx[work[i]] = kv[k];
+        w.poff[work[i]] = i;
+      }
+    }
+    if (tid == 0) w.poff[nuniq] = E;
   }
   if (tid == 0) {
-    w.poff[nuniq] = E;
     w.meta[0] = nuniq;
     w.meta[1] = ctl[0] ? 2 : 0;
     w.meta[3] = A.num_patches;
+    w.meta[4] = 0;  // arrival ticket of the iteration kernel
   }
   __syncthreads();
   trace(w.tmark, 41);
-  // per patch: free-pose mask, block count -> block offsets, per-position slots
+  // per patch: free-pose mask, block count -> block offsets
   for (int u = tid; u < nuniq; u += T) {
     unsigned mask = 0;
     for (int t = w.poff[u]; t < w.poff[u + 1]; t++) {
@@ -325,157 +376,12 @@ __device__ void ba_setup_phase(const BaArgs& A, const BaWs& w, char* lds, int P2
       const int p = __ffs(m) - 1;
       w.bpose[base + __popc(mask & ((1u << p) - 1u))] = p;
     }
-    for (int t = w.poff[u]; t < w.poff[u + 1]; t++) {
-      const int c = pij[t], ci = c & 0xff, cj = c >> 8;
-      const int si = ci != kNoPose ? __popc(mask & ((1u << ci) - 1u)) : 0xff;
-      const int sj = cj != kNoPose ? __popc(mask & ((1u << cj) - 1u)) : 0xff;
-      w.eslot[t] = si | (sj << 8);
-    }
   }
   if (tid == 0) {
     w.boff[nuniq] = nblocks;
     w.meta[2] = nblocks;
   }
-  if (N == 0) {
-    __syncthreads();
-    return;
-  }
-  __syncthreads();
   trace(w.tmark, 42);
-  // per-pose edge lists (position order): counts matrix [pose][thread] over
-  // contiguous position chunks, one scan, every thread fills its own cells
-  const int ch = (E + T - 1) / T, elo = min(tid * ch, E), ehi = min(elo + ch, E);
-  for (int p = 0; p < N; p++) work[p * T + tid] = 0;
-  for (int t = elo; t < ehi; t++) {
-    const int c = pij[t], ci = c & 0xff, cj = c >> 8;
-    if (ci != kNoPose) work[ci * T + tid]++;
-    if (cj != kNoPose && cj != ci) work[cj * T + tid]++;
-  }
-  __syncthreads();
-  int total = block_exclusive_scan(work, N * T, scr);
-  if (tid < N) w.eoff[tid] = work[tid * T];
-  if (tid == 0) w.eoff[N] = total;
-  __syncthreads();
-  for (int t = elo; t < ehi; t++) {
-    const int c = pij[t], ci = c & 0xff, cj = c >> 8;
-    if (ci != kNoPose) {
-      const int roles = 1 | ((cj == ci) ? 2 : 0);
-      const int other = (cj != ci) ? cj : kNoPose;
-      w.elist0[work[ci * T + tid]++] = (t << 8) | (other << 2) | roles;
-    }
-    if (cj != kNoPose && cj != ci) w.elist0[work[cj * T + tid]++] = (t << 8) | (ci << 2) | 2;
-  }
-  __syncthreads();
-  trace(w.tmark, 43);
-  // per-pose patch lists (patch order), same construction
-  const int cu = (nuniq + T - 1) / T, ulo = min(tid * cu, nuniq), uhi = min(ulo + cu, nuniq);
-  for (int p = 0; p < N; p++) work[p * T + tid] = 0;
-  for (int u = ulo; u < uhi; u++)
-    for (unsigned m = w.pmask[u]; m; m &= m - 1) work[(__ffs(m) - 1) * T + tid]++;
-  __syncthreads();
-  total = block_exclusive_scan(work, N * T, scr);
-  if (tid < N) w.qoff[tid] = work[tid * T];
-  if (tid == 0) w.qoff[N] = total;
-  __syncthreads();
-  for (int u = ulo; u < uhi; u++) {
-    const unsigned mask = w.pmask[u];
-    const int b0 = w.boff[u];
-    for (unsigned m = mask; m; m &= m - 1) {
-      const int p = __ffs(m) - 1;
-      w.qlist[work[p * T + tid]++] = make_int2(u, b0 + __popc(mask & ((1u << p) - 1u)));
-    }
-  }
-  __syncthreads();
-  trace(w.tmark, 44);
-  // pair ranges: one wave per pose a; stable partition of elist(a) by the
-  // other pose b < a (bucket a = "rest"), and of qlist(a) into one range per
-  // b < a of the patches that also touch b.  Wave ballots: deterministic.
-  for (int a = wid; a < N; a += kBaWaves) {
-    const int s0 = w.eoff[a], s1 = w.eoff[a + 1];
-    int cnt = 0;  // lane b: entries with other == b (lane a: the rest)
-    for (int base = s0; base < s1; base += 64) {
-      const int t = base + lane;
-      int o = (t < s1) ? ((w.elist0[t] >> 2) & 31) : -1;
-      if (t < s1 && o >= a) o = a;
-      for (int b = 0; b <= a; b++) {
-        const unsigned long long m = __ballot(o == b);
-        if (lane == b) cnt += __popcll(m);
-      }
-    }
-    int cur = s0 + wave_exclusive_scan(lane <= a ? cnt : 0, lane);
-    if (lane <= a) w.epair[a * kPairStride + lane] = cur;
-    for (int base = s0; base < s1; base += 64) {
-      const int t = base + lane;
-      const int ent = (t < s1) ? w.elist0[t] : 0;
-      int o = (t < s1) ? ((ent >> 2) & 31) : -1;
-      if (t < s1 && o >= a) o = a;
-      for (int b = 0; b <= a; b++) {
-        const unsigned long long m = __ballot(o == b);
-        if (m) {
-          const int pos = __shfl(cur, b, 64);
-          if (o == b) w.elist[pos + __popcll(m & lanemask_lt(lane))] = ent;
-          if (lane == b) cur += __popcll(m);
-        }
-      }
-    }
-  }
-  // qplist: a patch of qlist(a) lands in the range of every b < a in its mask
-  if (tid == 0) ctl[1] = 0;
-  __syncthreads();
-  trace(w.tmark, 45);
-  for (int a = wid; a < N; a += kBaWaves) {  // sizes first: ranges of all poses are stacked
-    const int s0 = w.qoff[a], s1 = w.qoff[a + 1];
-    int cnt = 0;
-    for (int base = s0; base < s1; base += 64) {
-      const int t = base + lane;
-      const unsigned mask = (t < s1) ? w.pmask[w.qlist[t].x] : 0u;
-      for (int b = 0; b < a; b++) {
-        const unsigned long long m = __ballot((mask >> b) & 1u);
-        if (lane == b) cnt += __popcll(m);
-      }
-    }
-    int tot = cnt;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-    if (lane == 0) work[a] = tot;
-    if (lane < a) work[kMaxFree + a * kPairStride + lane] = cnt;
-  }
-  __syncthreads();
-  if (tid < 64) {  // stack the per-pose ranges (poses in order)
-    int base = 0;
-    for (int a = 0; a < N; a++) {
-      const int c = (lane < a) ? work[kMaxFree + a * kPairStride + lane] : 0;
-      const int ex = wave_exclusive_scan(c, lane);
-      if (lane < a) work[kMaxFree + a * kPairStride + lane] = base + ex;
-      if (lane == 0) w.qpair[a * kPairStride + a] = base + work[a];
-      base += work[a];
-    }
-  }
-  __syncthreads();
-  for (int a = wid; a < N; a += kBaWaves) {
-    const int s0 = w.qoff[a], s1 = w.qoff[a + 1];
-    int cur = (lane < a) ? work[kMaxFree + a * kPairStride + lane] : 0;
-    if (lane < a) w.qpair[a * kPairStride + lane] = cur;
-    for (int base = s0; base < s1; base += 64) {
-      const int t = base + lane;
-      const int2 q = (t < s1) ? w.qlist[t] : make_int2(0, 0);
-      const unsigned mask = (t < s1) ? w.pmask[q.x] : 0u;
-      const int b0 = (t < s1) ? w.boff[q.x] : 0;
-      for (int b = 0; b < a; b++) {
-        const bool in = (mask >> b) & 1u;
-        const unsigned long long m = __ballot(in);
-        if (m) {
-          const int pos = __shfl(cur, b, 64);
-          if (in) {
-            const int sb = b0 + __popc(mask & ((1u << b) - 1u));
-            w.qplist[pos + __popcll(m & lanemask_lt(lane))] = make_int2(q.x, q.y | (sb << 16));
-          }
-          if (lane == b) cur += __popcll(m);
-        }
-      }
-    }
-  }
-  __syncthreads();
 }
 
 #pragma clang fp contract(off)
@@ -561,343 +467,276 @@ __global__ void reproject_kernel(const float* __restrict__ poses, const float* _
 }
 #pragma clang fp contract(fast)
 
-// linearize: thread per sorted position.  The restrict-qualified helper lets
-// the loads of both positions a thread owns issue before any store.
-__device__ __forceinline__ void linearize_positions(
-    const float* __restrict__ poses, const float* __restrict__ patches,
-    const float* __restrict__ intrinsics, const float* __restrict__ target,
-    const float* __restrict__ weight, const int4* __restrict__ srec, int E, int P, int kmax,
-    float* __restrict__ J, double* __restrict__ EC) {
-  const float fx = intrinsics[0], fy = intrinsics[1], cx = intrinsics[2], cy = intrinsics[3];
-#pragma unroll 2
-  for (int i = threadIdx.x; i < E; i += blockDim.x) {
-    const int4 r = srec[i];
-    const int e = r.x;
-    const int64_t kx = min(r.w, kmax);  // memory guard (reference: unchecked)
-    const float2 tg = reinterpret_cast<const float2*>(target)[e];
-    const float2 wt = reinterpret_cast<const float2*>(weight)[e];
+// ---------------------------------------------------------------------------
+// Per-patch linearisation shared by the Schur-block and patch-owner
+// workgroups: all edges of patch u (positions [poff[u], poff[u+1])).
+// ---------------------------------------------------------------------------
+struct Intr {
+  float fx, fy, cx, cy;
+};
+
+// edge at position t -> o[30] (w r Jz Ji Jj), pi/pj free-pose indices
+__device__ __forceinline__ void linearize_position(const BaArgs& A, const int4* __restrict__ srec,
+                                                   const Intr& K, int kmax, int t, float* o,
+                                                   int& pi, int& pj) {
+  const int4 r = srec[t];
+  const float2 tg = reinterpret_cast<const float2*>(A.target)[r.x];
+  const float2 wt = reinterpret_cast<const float2*>(A.weight)[r.x];
+  const int ix = min(max(r.y, 0), A.num_poses - 1);  // memory guard (reference: unchecked)
+  const int jx = min(max(r.z, 0), A.num_poses - 1);
+  edge_linearize(A.poses, A.patches, A.P, K.fx, K.fy, K.cx, K.cy, tg.x, tg.y, wt.x, wt.y, ix, jx,
+                 (int64_t)min(r.w, kmax), o);
+  pi = r.y - A.t0;
+  pj = r.z - A.t0;
+}
+
+// Schur block (a, b), a >= b, contributions of patch u, accumulated into
+// acc[36] (row-major 6x6) and yv[6] (diagonal blocks only).
+__device__ __forceinline__ void patch_schur_terms(const BaArgs& A, const BaWs& w, const Intr& K,
+                                                  int kmax, double lam, int u, int a, int b,
+                                                  double* acc, double* yv) {
+  const bool diag = a == b;
+  double C = 0.0, Uu = 0.0, ca[6], cc[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) ca[k] = cc[k] = 0.0;
+  const int t1 = w.poff[u + 1];
+  for (int t = w.poff[u]; t < t1; t++) {
     float o[30];
-    edge_linearize(poses, patches, P, fx, fy, cx, cy, tg.x, tg.y, wt.x, wt.y, r.y, r.z, kx, o);
-    float4* Jo = reinterpret_cast<float4*>(J + (size_t)kJStride * i);
+    int pi, pj;
+    linearize_position(A, w.srec, K, kmax, t, o, pi, pj);
 #pragma unroll
-    for (int k = 0; k < 7; k++) Jo[k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
-    reinterpret_cast<float2*>(Jo + 7)[0] = make_float2(o[28], o[29]);
-    double ec[14];
-#pragma unroll
-    for (int k = 0; k < 14; k++) ec[k] = 0.0;
-#pragma unroll
-    for (int row = 0; row < 2; row++) {  // ba_cuda.cu:352-373
+    for (int row = 0; row < 2; row++) {
       const double wr = o[row];
-      const float rr = o[2 + row], Jz = o[4 + row];
+      const float r = o[2 + row], Jz = o[4 + row];
+      const float* Ji = o + 6 + 6 * row;
+      const float* Jj = o + 18 + 6 * row;
       const double wz = wr * Jz;
+      C += wz * Jz;  // ba_cuda.cu:372-373
+      Uu += wr * r * Jz;
+      // E column blocks of poses a (and b) (:352-363)
+      if (pi == a)
 #pragma unroll
-      for (int k = 0; k < 6; k++) {
-        ec[k] -= wz * o[6 + 6 * row + k];
-        ec[6 + k] += wz * o[18 + 6 * row + k];
+        for (int k = 0; k < 6; k++) ca[k] -= wz * Ji[k];
+      if (pj == a)
+#pragma unroll
+        for (int k = 0; k < 6; k++) ca[k] += wz * Jj[k];
+      if (!diag) {
+        if (pi == b)
+#pragma unroll
+          for (int k = 0; k < 6; k++) cc[k] -= wz * Ji[k];
+        if (pj == b)
+#pragma unroll
+          for (int k = 0; k < 6; k++) cc[k] += wz * Jj[k];
       }
-      ec[12] += wz * Jz;
-      ec[13] += wr * rr * Jz;
-    }
-    double2* Eo = reinterpret_cast<double2*>(EC + (size_t)kEStride * i);
+      // B and v (:339-370)
+      if (diag) {
+        const double wrr = wr * r;
+        if (pi == a) {
 #pragma unroll
-    for (int k = 0; k < 7; k++) Eo[k] = make_double2(ec[2 * k], ec[2 * k + 1]);
-  }
-}
-
-__device__ void ba_linearize_phase(const BaArgs& A, const BaWs& w) {
-  linearize_positions(A.poses, A.patches, A.intrinsics, A.target, A.weight, w.srec, A.E, A.P,
-                      w.meta[3] - 1, w.J, w.EC);
-}
-
-// ---------------------------------------------------------------------------
-// PATCH: Q_u = 1/(C_u + lmbda), U_u, and c_{u,p} = sum of the E blocks of
-// pose p over the patch's edges (position = ascending edge order).
-// ---------------------------------------------------------------------------
-constexpr int kRegBlocks = 4;  // patches with <= 4 pose blocks accumulate in registers
-
-__device__ __forceinline__ void patch_sums(const int32_t* __restrict__ poff,
-                                           const int32_t* __restrict__ boff,
-                                           const int32_t* __restrict__ eslot,
-                                           const double* __restrict__ EC, double lam, int nuniq,
-                                           double* __restrict__ Q, double* __restrict__ U,
-                                           double* __restrict__ cb) {
-  for (int u = threadIdx.x; u < nuniq; u += blockDim.x) {
-    const int a = poff[u], b = poff[u + 1];
-    const int s0 = boff[u], nb = boff[u + 1] - s0;
-    double C = 0.0, Uu = 0.0, c[kRegBlocks][6];
+          for (int x = 0; x < 6; x++) {
+            const double wx = wr * Ji[x];
 #pragma unroll
-    for (int s = 0; s < kRegBlocks; s++)
-#pragma unroll
-      for (int k = 0; k < 6; k++) c[s][k] = 0.0;
-    for (int t = a; t < b; t++) {
-      const double2* ep = reinterpret_cast<const double2*>(EC + (size_t)kEStride * t);
-      double ec[14];
-#pragma unroll
-      for (int k = 0; k < 7; k++) {
-        const double2 v = ep[k];
-        ec[2 * k] = v.x;
-        ec[2 * k + 1] = v.y;
-      }
-      const int sl = eslot[t], si = sl & 0xff, sj = sl >> 8;
-      C += ec[12];
-      Uu += ec[13];
-#pragma unroll
-      for (int s = 0; s < kRegBlocks; s++) {
-        if (si == s)
-#pragma unroll
-          for (int k = 0; k < 6; k++) c[s][k] += ec[k];
-        if (sj == s)
-#pragma unroll
-          for (int k = 0; k < 6; k++) c[s][k] += ec[6 + k];
-      }
-    }
-    Q[u] = 1.0 / (C + lam);  // ba_cuda.cu:519
-    U[u] = Uu;
-    if (nb <= kRegBlocks) {
-#pragma unroll
-      for (int s = 0; s < kRegBlocks; s++) {
-        if (s < nb) {
-          double2* co = reinterpret_cast<double2*>(cb + 6 * (size_t)(s0 + s));
-          co[0] = make_double2(c[s][0], c[s][1]);
-          co[1] = make_double2(c[s][2], c[s][3]);
-          co[2] = make_double2(c[s][4], c[s][5]);
+            for (int z = 0; z < 6; z++) acc[6 * x + z] += wx * Ji[z];
+            yv[x] -= wrr * Ji[x];
+          }
         }
-      }
-    } else {
-      for (int s = 0; s < nb; s++) {  // rare: many poses on one patch
-        double cs[6] = {0, 0, 0, 0, 0, 0};
-        for (int t = a; t < b; t++) {
-          const double* ec = EC + (size_t)kEStride * t;
-          const int sl = eslot[t];
-          if ((sl & 0xff) == s)
+        if (pj == a) {
 #pragma unroll
-            for (int k = 0; k < 6; k++) cs[k] += ec[k];
-          if ((sl >> 8) == s)
+          for (int x = 0; x < 6; x++) {
+            const double wx = wr * Jj[x];
 #pragma unroll
-            for (int k = 0; k < 6; k++) cs[k] += ec[6 + k];
+            for (int z = 0; z < 6; z++) acc[6 * x + z] += wx * Jj[z];
+            yv[x] += wrr * Jj[x];
+          }
         }
+        if (pi == a && pj == a) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) cb[6 * (size_t)(s0 + s) + k] = cs[k];
+          for (int x = 0; x < 6; x++)
+#pragma unroll
+            for (int z = 0; z < 6; z++) acc[6 * x + z] -= wr * Ji[x] * Jj[z] + wr * Jj[x] * Ji[z];
+        }
+      } else {
+        if (pi == a && pj == b) {
+#pragma unroll
+          for (int x = 0; x < 6; x++) {
+            const double wx = wr * Ji[x];
+#pragma unroll
+            for (int z = 0; z < 6; z++) acc[6 * x + z] -= wx * Jj[z];
+          }
+        }
+        if (pj == a && pi == b) {
+#pragma unroll
+          for (int x = 0; x < 6; x++) {
+            const double wx = wr * Jj[x];
+#pragma unroll
+            for (int z = 0; z < 6; z++) acc[6 * x + z] -= wx * Ji[z];
+          }
+        }
       }
     }
   }
+  // - E Q E^T and - E Q u (:554-558)
+  const double q = 1.0 / (C + lam);
+  const double* cb = diag ? ca : cc;
+#pragma unroll
+  for (int x = 0; x < 6; x++) {
+    const double cq = ca[x] * q;
+#pragma unroll
+    for (int z = 0; z < 6; z++) acc[6 * x + z] -= cq * cb[z];
+  }
+  if (diag) {
+    const double qu = q * Uu;
+#pragma unroll
+    for (int x = 0; x < 6; x++) yv[x] -= ca[x] * qu;
+  }
 }
 
-__device__ void ba_patch_phase(const BaArgs& A, const BaWs& w) {
-  patch_sums(w.poff, w.boff, w.eslot, w.EC, (double)A.lmbda[0], w.meta[0], w.Q, w.U, w.cb);
+// Q_u, U_u and every c_{u,p} of patch u (patch-owner workgroups)
+__device__ __forceinline__ void patch_owner_terms(const BaArgs& A, const BaWs& w, const Intr& K,
+                                                  int kmax, double lam, int u) {
+  const int s0 = w.boff[u], nb = w.boff[u + 1] - s0;
+  const unsigned mask = w.pmask[u];
+  double C = 0.0, Uu = 0.0, c[kRegBlocks][6];
+#pragma unroll
+  for (int s = 0; s < kRegBlocks; s++)
+#pragma unroll
+    for (int k = 0; k < 6; k++) c[s][k] = 0.0;
+  const int t1 = w.poff[u + 1];
+  for (int t = w.poff[u]; t < t1; t++) {
+    float o[30];
+    int pi, pj;
+    linearize_position(A, w.srec, K, kmax, t, o, pi, pj);
+    const bool fi = pi >= 0 && pi < A.N, fj = pj >= 0 && pj < A.N;
+    const int si = fi ? __popc(mask & ((1u << pi) - 1u)) : -1;
+    const int sj = fj ? __popc(mask & ((1u << pj) - 1u)) : -1;
+#pragma unroll
+    for (int row = 0; row < 2; row++) {
+      const double wr = o[row];
+      const float r = o[2 + row], Jz = o[4 + row];
+      const double wz = wr * Jz;
+      C += wz * Jz;
+      Uu += wr * r * Jz;
+      if (nb <= kRegBlocks) {
+#pragma unroll
+        for (int s = 0; s < kRegBlocks; s++) {
+          if (si == s)
+#pragma unroll
+            for (int k = 0; k < 6; k++) c[s][k] -= wz * o[6 + 6 * row + k];
+          if (sj == s)
+#pragma unroll
+            for (int k = 0; k < 6; k++) c[s][k] += wz * o[18 + 6 * row + k];
+        }
+      } else {  // rare: many poses on one patch -> accumulate in place
+        double* cs = w.cb + 6 * (size_t)s0;
+        if (t == w.poff[u] && row == 0)
+          for (int k = 0; k < 6 * nb; k++) cs[k] = 0.0;
+        if (si >= 0)
+#pragma unroll
+          for (int k = 0; k < 6; k++) cs[6 * si + k] -= wz * o[6 + 6 * row + k];
+        if (sj >= 0)
+#pragma unroll
+          for (int k = 0; k < 6; k++) cs[6 * sj + k] += wz * o[18 + 6 * row + k];
+      }
+    }
+  }
+  w.Q[u] = 1.0 / (C + lam);  // ba_cuda.cu:519
+  w.U[u] = Uu;
+  if (nb <= kRegBlocks) {
+#pragma unroll
+    for (int s = 0; s < kRegBlocks; s++) {
+      if (s < nb) {
+        double2* co = reinterpret_cast<double2*>(w.cb + 6 * (size_t)(s0 + s));
+        co[0] = make_double2(c[s][0], c[s][1]);
+        co[1] = make_double2(c[s][2], c[s][3]);
+        co[2] = make_double2(c[s][4], c[s][5]);
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
-// SCHUR: S = B - E Q E^T (lower 6x6 blocks), y = v - E Q u.
+// Deterministic wave sum to lane 63 with DPP row shifts + row broadcasts
+// (no LDS traffic); fp64 values move as two 32-bit halves.
 // ---------------------------------------------------------------------------
+template <int CTRL, int ROW_MASK, int BANK_MASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, BANK_MASK, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, BANK_MASK, true);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double wave_sum_to_63(double v) {
+  v += dpp_f64<0x111, 0xf, 0xf>(v);  // row_shr:1
+  v += dpp_f64<0x112, 0xf, 0xf>(v);  // row_shr:2
+  v += dpp_f64<0x114, 0xf, 0xf>(v);  // row_shr:4
+  v += dpp_f64<0x118, 0xf, 0xf>(v);  // row_shr:8  -> lane 15 of each row: row sum
+  v += dpp_f64<0x142, 0xa, 0xf>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f64<0x143, 0xc, 0xf>(v);  // row_bcast:31 -> rows 2, 3: lane 63 = total
+  return v;
+}
+
+// sum of NV per-thread values over the workgroup, in a fixed order; the
+// result lands in red[0..NV) (LDS).  part: kIterWaves * NV doubles of LDS.
 template <int NV>
-__device__ __forceinline__ void team_reduce(double* v, int tau) {
-  for (int o = tau >> 1; o > 0; o >>= 1)
+__device__ __forceinline__ void block_sum(const double* v, double* part, double* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < NV; i++) v[i] += __shfl_xor(v[i], o, 64);
-}
-
-// diagonal block (a, a) and y_a; a full wave
-__device__ __forceinline__ void schur_diag(const int32_t* __restrict__ elist,
-                                           const int2* __restrict__ qlist,
-                                           const float* __restrict__ J,
-                                           const double* __restrict__ Q,
-                                           const double* __restrict__ U,
-                                           const double* __restrict__ cb, int e0, int e1, int q0,
-                                           int q1, int lane, double* Sb, double* ya) {
-  double acc[21], yv[6];
-#pragma unroll
-  for (int i = 0; i < 21; i++) acc[i] = 0.0;
-#pragma unroll
-  for (int i = 0; i < 6; i++) yv[i] = 0.0;
-#pragma unroll 2
-  for (int t = e0 + lane; t < e1; t += 64) {  // B_aa, v_a (ba_cuda.cu:339-370)
-    const int ent = elist[t];
-    const int roles = ent & 3;
-    const float4* o4 = reinterpret_cast<const float4*>(J + (size_t)kJStride * (ent >> 8));
-    float o[32];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const float4 v = o4[k];
-      o[4 * k] = v.x;
-      o[4 * k + 1] = v.y;
-      o[4 * k + 2] = v.z;
-      o[4 * k + 3] = v.w;
-    }
-#pragma unroll
-    for (int row = 0; row < 2; row++) {
-      const double wr = o[row];
-      const double wrr = wr * o[2 + row];
-      const float* ji = o + 6 + 6 * row;
-      const float* jv = o + 18 + 6 * row;
-      if (roles & 1) {
-#pragma unroll
-        for (int x = 0, q = 0; x < 6; x++) {
-          const double wx = wr * ji[x];
-#pragma unroll
-          for (int z = 0; z <= x; z++, q++) acc[q] += wx * ji[z];
-          yv[x] -= wrr * ji[x];
-        }
-      }
-      if (roles & 2) {
-#pragma unroll
-        for (int x = 0, q = 0; x < 6; x++) {
-          const double wx = wr * jv[x];
-#pragma unroll
-          for (int z = 0; z <= x; z++, q++) acc[q] += wx * jv[z];
-          yv[x] += wrr * jv[x];
-        }
-      }
-      if (roles == 3) {  // ii == jj: both cross terms land on the diagonal block
-#pragma unroll
-        for (int x = 0, q = 0; x < 6; x++)
-#pragma unroll
-          for (int z = 0; z <= x; z++, q++) acc[q] -= wr * ji[x] * jv[z] + wr * jv[x] * ji[z];
-      }
-    }
+  for (int i = 0; i < NV; i++) {
+    const double s = wave_sum_to_63(v[i]);
+    if (lane == 63) part[wid * NV + i] = s;
   }
-#pragma unroll 2
-  for (int t = q0 + lane; t < q1; t += 64) {  // E Q E^T, E Q u (:554-558)
-    const int2 qe = qlist[t];
-    const double2* cp = reinterpret_cast<const double2*>(cb + 6 * (size_t)qe.y);
-    const double2 c01 = cp[0], c23 = cp[1], c45 = cp[2];
-    const double c[6] = {c01.x, c01.y, c23.x, c23.y, c45.x, c45.y};
-    const double q = Q[qe.x], qu = q * U[qe.x];
-#pragma unroll
-    for (int x = 0, k = 0; x < 6; x++) {
-      const double cq = c[x] * q;
-#pragma unroll
-      for (int z = 0; z <= x; z++, k++) acc[k] -= cq * c[z];
-      yv[x] -= c[x] * qu;
-    }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double s = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); k++) s += part[k * NV + threadIdx.x];
+    red[threadIdx.x] = s;
   }
-  team_reduce<21>(acc, 64);
-  team_reduce<6>(yv, 64);
-#pragma unroll
-  for (int x = 0, k = 0; x < 6; x++)
-#pragma unroll
-    for (int z = 0; z <= x; z++, k++)
-      if (k == lane) {
-        Sb[6 * x + z] = acc[k];
-        Sb[6 * z + x] = acc[k];
-      }
-#pragma unroll
-  for (int x = 0; x < 6; x++)
-    if (21 + x == lane) ya[x] = yv[x];
-}
-
-// off-diagonal block (a, b), a > b: exactly the pair's edge and patch ranges
-__device__ __forceinline__ void schur_off(const int32_t* __restrict__ elist,
-                                          const int2* __restrict__ qplist,
-                                          const float* __restrict__ J,
-                                          const double* __restrict__ Q,
-                                          const double* __restrict__ cb, int e0, int e1, int q0,
-                                          int q1, int lane, int tau, double* Sb) {
-  double acc[36];
-#pragma unroll
-  for (int i = 0; i < 36; i++) acc[i] = 0.0;
-  for (int t = e0 + lane; t < e1; t += tau) {  // B_ab = -sum w J_a^T J_b
-    const int ent = elist[t];
-    // rows follow pose a: Ji when ii == a (roles bit 0), Jj when jj == a
-    const float* o = J + (size_t)kJStride * (ent >> 8);
-    const float* orow = o + ((ent & 1) ? 6 : 18);
-    const float* ocol = o + ((ent & 1) ? 18 : 6);
-#pragma unroll 1
-    for (int row = 0; row < 2; row++) {
-      const double wr = o[row];
-      float rx[6], cz[6];
-#pragma unroll
-      for (int k = 0; k < 6; k++) {
-        rx[k] = orow[6 * row + k];
-        cz[k] = ocol[6 * row + k];
-      }
-#pragma unroll
-      for (int x = 0; x < 6; x++) {
-        const double wx = wr * rx[x];
-#pragma unroll
-        for (int z = 0; z < 6; z++) acc[6 * x + z] -= wx * cz[z];
-      }
-    }
-  }
-  for (int t = q0 + lane; t < q1; t += tau) {
-    const int2 qe = qplist[t];
-    const double* ca = cb + 6 * (size_t)(qe.y & 0xffff);
-    const double* cc = cb + 6 * (size_t)(qe.y >> 16);
-    double va[6], vb[6];
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      va[k] = ca[k];
-      vb[k] = cc[k];
-    }
-    const double q = Q[qe.x];
-#pragma unroll
-    for (int x = 0; x < 6; x++) {
-      const double cq = va[x] * q;
-#pragma unroll
-      for (int z = 0; z < 6; z++) acc[6 * x + z] -= cq * vb[z];
-    }
-  }
-  team_reduce<36>(acc, tau);
-#pragma unroll
-  for (int k = 0; k < 36; k++)
-    if ((k % tau) == lane) Sb[k] = acc[k];
-}
-
-__device__ void ba_schur_phase(const BaWs& w, int N, double* Sout, double* yout) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int a = wid; a < N; a += kBaWaves)
-    schur_diag(w.elist, w.qlist, w.J, w.Q, w.U, w.cb, w.eoff[a], w.eoff[a + 1], w.qoff[a],
-               w.qoff[a + 1], lane, Sout + 36 * (size_t)blk(a, a), yout + 6 * a);
-  constexpr int tau = 16;
-  const int noff = N * (N - 1) / 2, nteam = blockDim.x / tau;
-  const int team = nteam - 1 - tid / tau, tl = tid % tau;
-  for (int d = team; d < noff; d += nteam) {
-    const int a = 1 + tri_row(d), b = d - a * (a - 1) / 2;  // a > b
-    schur_off(w.elist, w.qplist, w.J, w.Q, w.cb, w.epair[a * kPairStride + b],
-              w.epair[a * kPairStride + b + 1], w.qpair[a * kPairStride + b],
-              w.qpair[a * kPairStride + b + 1], tl, tau, Sout + 36 * (size_t)blk(a, b));
-  }
+  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
-// SOLVE: damped S (lower blocks, LDS) -> L in place; y -> dX in place.
-// rd[6k + c] = 1 / L_kk[c][c].
+// SOLVE tail (one workgroup): damped S (lower blocks in LDS) -> L in place,
+// y -> dX in place; rd[6k + c] = 1 / L_kk[c][c].
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double rsqrt_d(double x) {  // hardware estimate + 2 Newton steps
-  double r = __builtin_amdgcn_rsq(x);
-  const double h = 0.5 * x;
-  r = r * (1.5 - h * r * r);
-  r = r * (1.5 - h * r * r);
-  return r;
+__device__ __forceinline__ double rsqrt_d(double x) {  // estimate + one Newton step
+  const double r = __builtin_amdgcn_rsq(x);
+  return r * (1.5 - (0.5 * x) * r * r);
 }
 
-// one wave: Cholesky of the 6x6 pivot block, lane (r, c) = 6r + c holds
-// element (r, c); column steps broadcast through shuffles.
-__device__ __forceinline__ bool factor_pivot_block(double* Sb, double* rd) {
-  const int lane = threadIdx.x & 63, r6 = lane / 6, c6 = lane - 6 * (lane / 6);
-  const bool act = lane < 36;
-  double v = act ? Sb[lane] : 0.0;
+// one lane: Cholesky of a 6x6 pivot block held in registers
+__device__ __forceinline__ bool factor_block_lane(double* Sb, double* rd) {
+  double L[6][6];
+#pragma unroll
+  for (int r = 0; r < 6; r++)
+#pragma unroll
+    for (int c = 0; c <= r; c++) L[r][c] = Sb[6 * r + c];
   bool ok = true;
 #pragma unroll
   for (int c = 0; c < 6; c++) {
-    const double piv = __shfl(v, 7 * c, 64);
-    ok = ok && (piv > 0.0);
-    const double rs = rsqrt_d(piv);
-    if (act && c6 == c) v = (r6 == c) ? piv * rs : (r6 > c ? v * rs : v);
-    if (lane == c) rd[c] = rs;
-    const double lr = __shfl(v, min(6 * r6 + c, 63), 64);
-    const double lc = __shfl(v, min(6 * c6 + c, 63), 64);
-    if (act && c6 > c && r6 >= c6) v -= lr * lc;
+    const double d = L[c][c];
+    ok = ok && (d > 0.0);
+    const double rs = rsqrt_d(d);
+    rd[c] = rs;
+    L[c][c] = d * rs;
+#pragma unroll
+    for (int r = c + 1; r < 6; r++) L[r][c] *= rs;
+#pragma unroll
+    for (int c2 = c + 1; c2 < 6; c2++)
+#pragma unroll
+      for (int r = c2; r < 6; r++) L[r][c2] -= L[r][c] * L[c2][c];
   }
-  if (act) Sb[lane] = (c6 <= r6) ? v : 0.0;
+#pragma unroll
+  for (int r = 0; r < 6; r++)
+#pragma unroll
+    for (int c = 0; c < 6; c++) Sb[6 * r + c] = c <= r ? L[r][c] : 0.0;
   return ok;
 }
 
 // row r of block (a, b) -= row r of L_ak times L_bk^T
 __device__ __forceinline__ void trailing_row(double* S, int k, int a, int b, int r) {
-  const double* la = S + 36 * (size_t)blk(a, k) + 6 * r;
-  const double* lb = S + 36 * (size_t)blk(b, k);
-  double* row = S + 36 * (size_t)blk(a, b) + 6 * r;
+  const double* la = S + 36 * blk(a, k) + 6 * r;
+  const double* lb = S + 36 * blk(b, k);
+  double* row = S + 36 * blk(a, b) + 6 * r;
   double lr[6];
 #pragma unroll
   for (int q = 0; q < 6; q++) lr[q] = la[q];
@@ -910,53 +749,51 @@ __device__ __forceinline__ void trailing_row(double* S, int k, int a, int b, int
   }
 }
 
-__device__ void ba_solve_phase(int N, double* S, double* rd, double* y, int* fail,
-                               int64_t* tr = nullptr) {
+__device__ void ba_solve(int N, double* S, double* rd, double* y, int* fail, int64_t* tr) {
   const int tid = threadIdx.x, T = blockDim.x, wid = tid >> 6, lane = tid & 63;
   for (int t = tid; t < 6 * N; t += T) {  // S += I * (1e-4 S + 1)  (ba_cuda.cu:560)
-    double* d = S + 36 * (size_t)blk(t / 6, t / 6) + 7 * (t % 6);
+    double* d = S + 36 * blk(t / 6, t / 6) + 7 * (t % 6);
     *d += 1e-4 * *d + 1.0;
   }
   __syncthreads();
-  if (wid == 0) {
-    const bool ok = factor_pivot_block(S, rd);
-    if (lane == 0) *fail = ok ? 0 : 1;
-  }
+  if (tid == 0) *fail = factor_block_lane(S, rd) ? 0 : 1;
   __syncthreads();
   trace(tr, 50);
   for (int k = 0; k < N; k++) {
     const int m = N - k - 1;
-    // panel: L_ak = S_ak L_kk^{-T} by substitution, one row per thread
-    {
-      const double* Lkk = S + 36 * (size_t)blk(k, k);
-      const double* rk = rd + 6 * k;
+    {  // panel: L_ak = S_ak L_kk^{-T}, right-looking substitution per row
+      const double* Lkk = S + 36 * blk(k, k);
+      double lk[6][6], rk[6];
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        rk[c] = rd[6 * k + c];
+#pragma unroll
+        for (int q = 0; q < c; q++) lk[c][q] = Lkk[6 * c + q];
+      }
       for (int t = tid; t < 6 * m; t += T) {
         const int a = k + 1 + t / 6, r = t % 6;
-        double* row = S + 36 * (size_t)blk(a, k) + 6 * r;
+        double* row = S + 36 * blk(a, k) + 6 * r;
         double x[6];
 #pragma unroll
         for (int c = 0; c < 6; c++) x[c] = row[c];
 #pragma unroll
         for (int c = 0; c < 6; c++) {
-          double s = x[c];
+          x[c] *= rk[c];
 #pragma unroll
-          for (int q = 0; q < c; q++) s -= x[q] * Lkk[6 * c + q];
-          x[c] = s * rk[c];
+          for (int c2 = c + 1; c2 < 6; c2++) x[c2] -= x[c] * lk[c2][c];
         }
 #pragma unroll
         for (int c = 0; c < 6; c++) row[c] = x[c];
       }
     }
     __syncthreads();
-    trace(tr, 51 + 2 * k);
     if (m == 0) break;
     // trailing update; wave 0 takes block (k+1, k+1) and factors it right
     // away (look-ahead) while the other waves update the rest
     if (wid == 0) {
       if (lane < 6) trailing_row(S, k, k + 1, k + 1, lane);
       wave_lds_sync();
-      const bool ok = factor_pivot_block(S + 36 * (size_t)blk(k + 1, k + 1), rd + 6 * (k + 1));
-      if (!ok && lane == 0) *fail = 1;
+      if (lane == 0 && !factor_block_lane(S + 36 * blk(k + 1, k + 1), rd + 6 * (k + 1))) *fail = 1;
     } else {
       const int ntask = 6 * (m * (m + 1) / 2 - 1);
       for (int t = tid - 64; t < ntask; t += T - 64) {
@@ -966,31 +803,32 @@ __device__ void ba_solve_phase(int N, double* S, double* rd, double* y, int* fai
       }
     }
     __syncthreads();
-    trace(tr, 52 + 2 * k);
   }
+  trace(tr, 51);
   if (*fail) {
     for (int t = tid; t < 6 * N; t += T) y[t] = 0.0;  // dX = 0 (dpvo/ba.py:17-21)
   } else if (wid == 0) {
-    // forward: z_k = L_kk^{-1} y_k, then y_a -= L_ak z_k (a > k); every lane
-    // keeps z_k in registers
+    // forward: z_k = L_kk^{-1} y_k, then y_a -= L_ak z_k (a > k)
     for (int k = 0; k < N; k++) {
-      const double* Lkk = S + 36 * (size_t)blk(k, k);
+      const double* Lkk = S + 36 * blk(k, k);
       double z[6];
 #pragma unroll
-      for (int r = 0; r < 6; r++) {
-        double s = y[6 * k + r];
+      for (int c = 0; c < 6; c++) z[c] = y[6 * k + c];
 #pragma unroll
-        for (int q = 0; q < r; q++) s -= Lkk[6 * r + q] * z[q];
-        z[r] = s * rd[6 * k + r];
+      for (int c = 0; c < 6; c++) {
+        z[c] *= rd[6 * k + c];
+#pragma unroll
+        for (int c2 = c + 1; c2 < 6; c2++) z[c2] -= z[c] * Lkk[6 * c2 + c];
       }
       for (int t = lane; t < 6 * (N - k - 1); t += 64) {
         const int a = k + 1 + t / 6, r = t % 6;
-        const double* la = S + 36 * (size_t)blk(a, k) + 6 * r;
+        const double* la = S + 36 * blk(a, k) + 6 * r;
         double v = y[6 * a + r];
 #pragma unroll
         for (int c = 0; c < 6; c++) v -= la[c] * z[c];
         y[6 * a + r] = v;
       }
+      wave_lds_sync();
 #pragma unroll
       for (int r = 0; r < 6; r++)
         if (lane == r) y[6 * k + r] = z[r];
@@ -998,23 +836,25 @@ __device__ void ba_solve_phase(int N, double* S, double* rd, double* y, int* fai
     }
     // backward: x_k = L_kk^{-T} z_k, then z_b -= L_kb^T x_k (b < k)
     for (int k = N - 1; k >= 0; k--) {
-      const double* Lkk = S + 36 * (size_t)blk(k, k);
+      const double* Lkk = S + 36 * blk(k, k);
       double x[6];
 #pragma unroll
-      for (int r = 5; r >= 0; r--) {
-        double s = y[6 * k + r];
+      for (int c = 0; c < 6; c++) x[c] = y[6 * k + c];
 #pragma unroll
-        for (int q = r + 1; q < 6; q++) s -= Lkk[6 * q + r] * x[q];
-        x[r] = s * rd[6 * k + r];
+      for (int c = 5; c >= 0; c--) {
+        x[c] *= rd[6 * k + c];
+#pragma unroll
+        for (int c2 = 0; c2 < c; c2++) x[c2] -= x[c] * Lkk[6 * c + c2];
       }
       for (int t = lane; t < 6 * k; t += 64) {
         const int b = t / 6, r = t % 6;
-        const double* lk = S + 36 * (size_t)blk(k, b);
+        const double* lk = S + 36 * blk(k, b);
         double v = y[6 * b + r];
 #pragma unroll
         for (int c = 0; c < 6; c++) v -= lk[6 * c + r] * x[c];
         y[6 * b + r] = v;
       }
+      wave_lds_sync();
 #pragma unroll
       for (int r = 0; r < 6; r++)
         if (lane == r) y[6 * k + r] = x[r];
@@ -1022,43 +862,14 @@ __device__ void ba_solve_phase(int N, double* S, double* rd, double* y, int* fai
     }
   }
   __syncthreads();
+  trace(tr, 52);
 }
 
 // ---------------------------------------------------------------------------
 // UPDATE: pose_retr_kernel (:178-206), dZ (:563), patch_retr_kernel (:209-229)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void patch_retract(const int32_t* __restrict__ boff,
-                                              const int32_t* __restrict__ bpose,
-                                              const double* __restrict__ cb,
-                                              const double* __restrict__ Q,
-                                              const double* __restrict__ U,
-                                              const int64_t* __restrict__ kx, const double* x,
-                                              int nuniq, int P, float* __restrict__ patches) {
-  for (int u = threadIdx.x; u < nuniq; u += blockDim.x) {
-    double s = U[u];
-    for (int b = boff[u]; b < boff[u + 1]; b++) {
-      const int p = bpose[b];
-      const double2* c = reinterpret_cast<const double2*>(cb + 6 * (size_t)b);
-      const double2 c01 = c[0], c23 = c[1], c45 = c[2];
-      const double* xp = x + 6 * p;
-      s -= c01.x * xp[0];
-      s -= c01.y * xp[1];
-      s -= c23.x * xp[2];
-      s -= c23.y * xp[3];
-      s -= c45.x * xp[4];
-      s -= c45.y * xp[5];
-    }
-    const float dz = (float)(Q[u] * s);
-    float* pk = patches + (size_t)kx[u] * 3 * P * P + 2 * P * P;
-    float d = pk[0] + dz;
-    d = (d > 20.0f) ? 1.0f : d;
-    d = (float)fmax((double)d, 1e-4);
-    for (int k = 0; k < P * P; k++) pk[k] = d;
-  }
-}
-
-__device__ void ba_update_phase(const BaArgs& A, const BaWs& w, const double* x, int fail,
-                                double* dX_out) {
+__device__ void ba_update(const BaArgs& A, const BaWs& w, const double* x, int fail,
+                          double* dX_out) {
   const int tid = threadIdx.x, T = blockDim.x, N = A.N;
   for (int i = tid; i < 6 * N; i += T) {
     w.dX[i] = x[i];
@@ -1077,91 +888,113 @@ __device__ void ba_update_phase(const BaArgs& A, const BaWs& w, const double* x,
     pt[0] = t1[0]; pt[1] = t1[1]; pt[2] = t1[2];
     pt[3] = q1[0]; pt[4] = q1[1]; pt[5] = q1[2]; pt[6] = q1[3];
   }
-  patch_retract(w.boff, w.bpose, w.cb, w.Q, w.U, w.kx, x, w.meta[0], A.P, A.patches);
+  const int nuniq = w.meta[0], P = A.P;
+  for (int u = tid; u < nuniq; u += T) {
+    double s = w.U[u];
+    for (int b = w.boff[u]; b < w.boff[u + 1]; b++) {
+      const double2* c = reinterpret_cast<const double2*>(w.cb + 6 * (size_t)b);
+      const double2 c01 = c[0], c23 = c[1], c45 = c[2];
+      const double* xp = x + 6 * w.bpose[b];
+      s -= c01.x * xp[0];
+      s -= c01.y * xp[1];
+      s -= c23.x * xp[2];
+      s -= c23.y * xp[3];
+      s -= c45.x * xp[4];
+      s -= c45.y * xp[5];
+    }
+    const float dz = (float)(w.Q[u] * s);
+    float* pk = A.patches + (size_t)w.kx[u] * 3 * P * P + 2 * P * P;
+    float d = pk[0] + dz;
+    d = (d > 20.0f) ? 1.0f : d;
+    d = (float)fmax((double)d, 1e-4);
+    for (int k = 0; k < P * P; k++) pk[k] = d;
+  }
 }
 
-// LDS carve of the solve region
-struct SolveLds {
-  int* ctl;
+struct IterLds {
+  int* ctl;  // [0] last-arrival flag, [1] Cholesky failure
   double* S;
   double* rd;
   double* y;
+  double* part;  // kIterWaves x 42
 };
-__device__ __forceinline__ SolveLds solve_carve(char* lds, int N) {
-  SolveLds s;
+__device__ __forceinline__ IterLds iter_carve(char* lds, int N) {
+  IterLds s;
   s.ctl = reinterpret_cast<int*>(lds);
   s.S = reinterpret_cast<double*>(lds + kCtlBytes);
   s.rd = s.S + 36 * (N * (N + 1) / 2);
   s.y = s.rd + 6 * N;
+  s.part = s.y + 6 * N;
   return s;
 }
 
-// one BA call: setup + all iterations in one workgroup.  Thread 0 stamps
-// the 100 MHz wall clock after every phase (dpvo_ba_phase_marks).
-__device__ __forceinline__ void mark(const BaWs& w, int slot) {
-  if (threadIdx.x == 0 && slot < 38) w.tmark[slot] = (int64_t)wall_clock64();
-}
-
-__global__ void __launch_bounds__(kBaThreads)
-    ba_fused_kernel(BaArgs A, BaWs w, int P2, int iterations) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  mark(w, 0);
-  if (threadIdx.x == 0) w.tmark[38] = (int64_t)clock64();
-  ba_setup_phase(A, w, lds, P2);
-  mark(w, 1);
-  const SolveLds L = solve_carve(lds, A.N);
-  for (int it = 0; it < iterations; it++) {
-    const int m0 = 2 + 5 * it;
-    ba_linearize_phase(A, w);
-    __syncthreads();
-    mark(w, m0);
-    ba_patch_phase(A, w);
-    __syncthreads();
-    mark(w, m0 + 1);
-    int fail = 0;
-    if (A.N > 0) {
-      ba_schur_phase(w, A.N, L.S, L.y);
-      __syncthreads();
-      mark(w, m0 + 2);
-      ba_solve_phase(A.N, L.S, L.rd, L.y, L.ctl + 1, it == 0 ? w.tmark : nullptr);
-      fail = L.ctl[1];
-    }
-    mark(w, m0 + 3);
-    ba_update_phase(A, w, L.y, fail, nullptr);
-    __syncthreads();
-    mark(w, m0 + 4);
-  }
-  if (threadIdx.x == 0) w.tmark[39] = (int64_t)clock64();
-}
-
-__global__ void __launch_bounds__(kBaThreads) ba_setup_kernel(BaArgs A, BaWs w, int P2) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  ba_setup_phase(A, w, lds, P2);
-}
-
-__global__ void __launch_bounds__(kBaThreads)
-    ba_build_kernel(BaArgs A, BaWs w, double* S_out, double* y_out) {
-  ba_linearize_phase(A, w);
-  __syncthreads();
-  ba_patch_phase(A, w);
-  __syncthreads();
-  if (A.N > 0) ba_schur_phase(w, A.N, S_out, y_out);
-}
-
-__global__ void __launch_bounds__(kBaThreads)
-    ba_solve_kernel(BaArgs A, BaWs w, const double* S_in, const double* y_in, double* dX_out) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const SolveLds L = solve_carve(lds, A.N);
+// the solve tail: S, y from global -> LDS, factor, substitute, update
+__device__ void ba_solve_tail(const BaArgs& A, const BaWs& w, const double* S_in,
+                              const double* y_in, double* dX_out, const IterLds& L, int64_t* tr) {
   const int N = A.N, NL = N * (N + 1) / 2;
   int fail = 0;
   if (N > 0) {
     for (int t = threadIdx.x; t < 36 * NL; t += blockDim.x) L.S[t] = S_in[t];
     for (int t = threadIdx.x; t < 6 * N; t += blockDim.x) L.y[t] = y_in[t];
     __syncthreads();
-    ba_solve_phase(N, L.S, L.rd, L.y, L.ctl + 1);
+    ba_solve(N, L.S, L.rd, L.y, L.ctl + 1, tr);
     fail = L.ctl[1];
   }
-  ba_update_phase(A, w, L.y, fail, dX_out);
+  ba_update(A, w, L.y, fail, dX_out);
+}
+
+// One F-BA iteration.  blockIdx < NL: Schur block; then patch owners; the
+// last workgroup to finish (when do_solve) runs the solve tail.
+__global__ void __launch_bounds__(kIterThreads)
+    ba_iter_kernel(BaArgs A, BaWs w, double* S_out, double* y_out, double* dX_out, int do_solve,
+                   int trace_it) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const IterLds L = iter_carve(lds, A.N);
+  const int N = A.N, NL = N * (N + 1) / 2, tid = threadIdx.x;
+  const Intr K{A.intrinsics[0], A.intrinsics[1], A.intrinsics[2], A.intrinsics[3]};
+  const int kmax = w.meta[3] - 1;
+  const double lam = (double)A.lmbda[0];
+  const int nuniq = w.meta[0];
+  int64_t* tr = trace_it ? w.tmark : nullptr;
+  if (tid == 0) w.wgt[2 * blockIdx.x] = (int64_t)wall_clock64();
+  if ((int)blockIdx.x < NL) {
+    const int d = blockIdx.x, a = tri_row(d), b = d - a * (a + 1) / 2;
+    double acc[42];  // 36 S entries + 6 y entries
+#pragma unroll
+    for (int i = 0; i < 42; i++) acc[i] = 0.0;
+    for (int u = tid; u < nuniq; u += blockDim.x) {
+      const unsigned mask = w.pmask[u];
+      if (((mask >> a) & 1u) && ((mask >> b) & 1u))
+        patch_schur_terms(A, w, K, kmax, lam, u, a, b, acc, acc + 36);
+    }
+    block_sum<42>(acc, L.part, L.S);
+    if (tid < 36) S_out[36 * d + tid] = L.S[tid];
+    if (a == b && tid >= 36 && tid < 42) y_out[6 * a + tid - 36] = L.S[tid];
+  } else {
+    const int u = (blockIdx.x - NL) * blockDim.x + tid;
+    if (u < nuniq) patch_owner_terms(A, w, K, kmax, lam, u);
+  }
+  __syncthreads();
+  if (tid == 0) w.wgt[2 * blockIdx.x + 1] = (int64_t)wall_clock64();
+  if (!do_solve) return;
+  // last-arrival election: release this workgroup's writes, take a ticket
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) L.ctl[0] = (atomicAdd(&w.meta[4], 1) == (int)gridDim.x - 1) ? 1 : 0;
+  __syncthreads();
+  if (!L.ctl[0]) return;
+  __threadfence();  // acquire: every other workgroup's S blocks, Q, U, c
+  trace(tr, 49);
+  ba_solve_tail(A, w, S_out, y_out, dX_out, L, tr);
+  if (tid == 0) w.meta[4] = 0;  // ticket for the next launch
+}
+
+// split form, step 3: solve + update from an (all-reduced) S, y
+__global__ void __launch_bounds__(kIterThreads)
+    ba_solve_kernel(BaArgs A, BaWs w, const double* S_in, const double* y_in, double* dX_out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const IterLds L = iter_carve(lds, A.N);
+  ba_solve_tail(A, w, S_in, y_in, dX_out, L, nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1213,13 +1046,12 @@ using namespace dpvo;
 static void ensure_lds_limits() {
   static bool done = false;
   if (done) return;
-  const int big = 160 * 1024;
-  (void)hipFuncSetAttribute((const void*)ba_fused_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, big);
   (void)hipFuncSetAttribute((const void*)ba_setup_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, big);
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kSetupLds);
+  (void)hipFuncSetAttribute((const void*)ba_iter_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)ba_solve_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, big);
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   done = true;
 }
 
@@ -1252,6 +1084,8 @@ static BaArgs make_args(float* poses, float* patches, const float* intrinsics, c
   return a;
 }
 
+static int iter_grid(int E, int N) { return N * (N + 1) / 2 + (E + kIterThreads - 1) / kIterThreads; }
+
 DPVO_EXPORT size_t dpvo_ba_workspace_bytes(int E, int t0, int t1) {
   const int N = t1 > t0 ? t1 - t0 : 0;
   return ba_layout(E > 0 ? E : 1, N, nullptr, nullptr);
@@ -1270,11 +1104,10 @@ DPVO_EXPORT int dpvo_ba_setup(const int64_t* ii, const int64_t* jj, const int64_
   BaWs w;
   ba_layout(E, N, (char*)workspace, &w);
   ensure_lds_limits();
-  const int P2 = pow2_at_least(E < 2 ? 2 : E);
   BaArgs a = make_args(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, ii, jj, kk, E, 0, 0,
                        num_patches, t0, t1);
-  hipLaunchKernelGGL(ba_setup_kernel, dim3(1), dim3(kBaThreads), setup_lds(P2, N),
-                     as_stream(stream), a, w, P2);
+  hipLaunchKernelGGL(ba_setup_kernel, dim3(1), dim3(kSetupThreads), kSetupLds, as_stream(stream),
+                     a, w, pow2_at_least(E < 2 ? 2 : E));
   return launch_status();
 }
 
@@ -1290,11 +1123,11 @@ DPVO_EXPORT int dpvo_ba_build_schur(const float* poses, const float* patches,
   if (N > kMaxFree || E > kMaxSetupE) return DPVO_ERR_UNSUPPORTED;
   BaWs w;
   ba_layout(E, N, (char*)workspace, &w);
-  // kk is clamped against the patch count the setup recorded on the device
+  ensure_lds_limits();
   BaArgs a = make_args(const_cast<float*>(poses), const_cast<float*>(patches), intrinsics, target,
                        weight, lmbda, ii, jj, kk, E, P, num_poses, 0, t0, t1);
-  hipLaunchKernelGGL(ba_build_kernel, dim3(1), dim3(kBaThreads), 0, as_stream(stream), a, w,
-                     S_lower ? S_lower : w.S, y ? y : w.y);
+  hipLaunchKernelGGL(ba_iter_kernel, dim3(iter_grid(E, N)), dim3(kIterThreads), iter_lds(N),
+                     as_stream(stream), a, w, S_lower ? S_lower : w.S, y ? y : w.y, nullptr, 0, 0);
   return launch_status();
 }
 
@@ -1310,7 +1143,7 @@ DPVO_EXPORT int dpvo_ba_solve_update(float* poses, float* patches, const double*
   ensure_lds_limits();
   BaArgs a = make_args(poses, patches, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                        nullptr, E, P, num_poses, 0, t0, t1);
-  hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(kBaThreads), solve_lds(N), as_stream(stream),
+  hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(kIterThreads), iter_lds(N), as_stream(stream),
                      a, w, S_lower ? S_lower : w.S, y ? y : w.y, dX_out);
   return launch_status();
 }
@@ -1326,13 +1159,26 @@ DPVO_EXPORT int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1
              : DPVO_ERR_LAUNCH;
 }
 
-DPVO_EXPORT int dpvo_ba_phase_marks(const void* workspace, int E, int t0, int t1,
-                                    int64_t* out, void* stream) {
+DPVO_EXPORT int dpvo_ba_phase_marks(const void* workspace, int E, int t0, int t1, int64_t* out,
+                                    void* stream) {
   if (!workspace || !out || E <= 0) return DPVO_ERR_INVALID;
   BaWs w;
   ba_layout(E, t1 > t0 ? t1 - t0 : 0, (char*)workspace, &w);
   return hipMemcpyAsync(out, w.tmark, sizeof(int64_t) * kMarks, hipMemcpyDeviceToDevice,
                         as_stream(stream)) == hipSuccess
+             ? DPVO_OK
+             : DPVO_ERR_LAUNCH;
+}
+
+// instrumentation: per-workgroup start/end stamps of the last iteration launch
+DPVO_EXPORT int dpvo_ba_workgroup_marks(const void* workspace, int E, int t0, int t1, int64_t* out,
+                                        void* stream) {
+  if (!workspace || !out || E <= 0) return DPVO_ERR_INVALID;
+  const int N = t1 > t0 ? t1 - t0 : 0;
+  BaWs w;
+  ba_layout(E, N, (char*)workspace, &w);
+  return hipMemcpyAsync(out, w.wgt, sizeof(int64_t) * 2 * iter_grid(E, N),
+                        hipMemcpyDeviceToDevice, as_stream(stream)) == hipSuccess
              ? DPVO_OK
              : DPVO_ERR_LAUNCH;
 }
@@ -1355,13 +1201,18 @@ DPVO_EXPORT int dpvo_ba_forward(float* poses, float* patches, const float* intri
   BaWs w;
   ba_layout(E, N, (char*)workspace, &w);
   ensure_lds_limits();
-  const int P2 = pow2_at_least(E < 2 ? 2 : E);
-  const size_t a = setup_lds(P2, N), b = solve_lds(N);
-  BaArgs args = make_args(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
-                          num_poses, num_patches, t0, t1);
-  hipLaunchKernelGGL(ba_fused_kernel, dim3(1), dim3(kBaThreads), (a > b ? a : b),
-                     as_stream(stream), args, w, P2, iterations);
-  return launch_status();
+  hipStream_t s = as_stream(stream);
+  BaArgs a = make_args(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
+                       num_poses, num_patches, t0, t1);
+  hipLaunchKernelGGL(ba_setup_kernel, dim3(1), dim3(kSetupThreads), kSetupLds, s, a, w,
+                     pow2_at_least(E < 2 ? 2 : E));
+  int st = launch_status();
+  for (int it = 0; it < iterations && st == DPVO_OK; it++) {
+    hipLaunchKernelGGL(ba_iter_kernel, dim3(iter_grid(E, N)), dim3(kIterThreads), iter_lds(N), s,
+                       a, w, w.S, w.y, nullptr, 1, it == 0 ? 1 : 0);
+    st = launch_status();
+  }
+  return st;
 }
 
 DPVO_EXPORT int dpvo_reproject(const float* poses, const float* patches, const float* intrinsics,

@@ -141,6 +141,10 @@ int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1, int* out, 
    shader clock: [38] start, [39] end; [40..] finer stamps inside the setup
    and the first solve -- copied to the DEVICE array `out`. */
 int dpvo_ba_phase_marks(const void* workspace, int E, int t0, int t1, int64_t* out, void* stream);
+/* Instrumentation: start / end wall-clock stamps of every workgroup of the
+   last iteration launch, [2 x (N(N+1)/2 + ceil(E/512))] int64 to DEVICE `out`. */
+int dpvo_ba_workgroup_marks(const void* workspace, int E, int t0, int t1, int64_t* out,
+                            void* stream);
 
 /* F-REPROJ.  Replaces cuda_ba.reproject (ba.cpp:47-53 -> cuda_reproject,
    ba_cuda.cu:585-616 + reproject :379-429).  coords [E,2,P,P]. */

@@ -1,5 +1,7 @@
-"""Per-phase timing of the fused F-BA kernel (GPU): wall-clock marks stamped
-by thread 0 after every phase (cuda_ba.forward_marks), medians over reps.
+"""Timing of one F-BA call (GPU): CUDA-event total per call, plus the
+wall-clock stamps the kernels leave in the workspace (cuda_ba.forward_marks):
+setup start/sort/end, and in iteration 0 the solve tail (start, first
+factor, factorisation, substitution).
 
     python scripts/ba_phases.py [cfg] [iterations]
 """
@@ -18,43 +20,39 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 G = synthetic.make_config(cfg, seed=0)
 D = G.to(dev)
-N = G.F - 1
 lm = torch.tensor([1e-4], device=dev)
-names = ["linearize", "patch", "schur", "solve", "update"]
 acc = {}
-for rep in range(25):
+for rep in range(30):
     poses, patches = D.poses.clone(), D.patches.clone()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    cb.forward(poses, patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj, D.kk, G.M, 1,
+               G.F, iters, False)
+    e1.record()
+    torch.cuda.synchronize()
     m = cb.forward_marks(poses, patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj, D.kk,
                          G.M, 1, G.F, iters, False).cpu().tolist()
     if rep < 5:
         continue
-    d = {}
-    prev = m[0]
-    for k, slot in [("sort", 40), ("ranks", 41), ("masks+slots", 42), ("elists", 43),
-                    ("qlists", 44), ("epart", 45), ("qpart", 1)]:
-        d["setup." + k] = m[slot] - prev
-        prev = m[slot]
-    for it in range(iters):
-        for k, n in enumerate(names):
-            t = m[2 + 5 * it + k]
-            if it == 0 and n == "solve":  # fine stamps of the first solve
-                p2 = m[4]
-                d["solve.factor0"] = m[50] - p2
-                p2 = m[50]
-                for kk in range(N):
-                    d[f"solve.panel{kk}"] = m[51 + 2 * kk] - p2
-                    p2 = m[51 + 2 * kk]
-                    if kk < N - 1:
-                        d[f"solve.trail{kk}"] = m[52 + 2 * kk] - p2
-                        p2 = m[52 + 2 * kk]
-                d["solve.subst"] = t - p2
-            d[f"{n}{it}"] = t - prev
-            prev = t
-    d["total"] = prev - m[0]
+    d = {"call (events)": e0.elapsed_time(e1) * 1e3}
+    for name, a, b in [("setup.sort", 40, 41), ("setup.masks", 41, 42),
+                       ("setup -> solve tail", 42, 49), ("solve.factor0", 49, 50),
+                       ("solve.factorise", 50, 51), ("solve.substitute", 51, 52)]:
+        d[name] = (m[b] - m[a]) * 10.0 / 1000.0
+    wg = m[64:]
+    NL = (G.F - 1) * G.F // 2
+    starts, ends = wg[0::2], wg[1::2]
+    t0 = min(starts)
+    dur = [(e - s) * 0.01 for s, e in zip(starts, ends)]
+    d["iter: first WG start -> last WG end"] = (max(ends) - t0) * 0.01
+    d["iter: diag WG max dur"] = max(dur[i] for i in range(NL)
+                                     if i == (int((8 * i + 1) ** 0.5 - 1) // 2) *
+                                     ((int((8 * i + 1) ** 0.5 - 1) // 2) + 3) // 2)
+    d["iter: off WG max dur"] = max(dur[:NL])
+    d["iter: owner WG max dur"] = max(dur[NL:])
+    d["iter: WG start spread"] = (max(starts) - t0) * 0.01
     for k, v in d.items():
-        acc.setdefault(k, []).append(v * 10.0 / 1000.0)  # 100 MHz ticks -> us
-    # shader clock cycles / wall time: the core clock the kernel ran at
-    acc.setdefault("clock_MHz", []).append((m[39] - m[38]) / max(1, prev - m[0]) * 100.0)
+        acc.setdefault(k, []).append(v)
 for k, v in acc.items():
     v.sort()
-    print(f"{k:16s} median {v[len(v) // 2]:8.2f}", "MHz" if k == "clock_MHz" else "us")
+    print(f"{k:22s} median {v[len(v) // 2]:8.2f} us")
