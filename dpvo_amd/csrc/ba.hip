@@ -43,26 +43,27 @@ constexpr int kMaxFree = 20;  // pose-block masks are 32-bit; lower S blocks of 
 constexpr int kPerThread = kMaxSetupE / kSetupThreads;
 constexpr int kCtlBytes = 512;
 constexpr int kSetupLds = 160 * 1024;
-constexpr int kMarks = 64;
+constexpr int kMarks = 128;
 constexpr int kNoPose = 31;
-constexpr int kRegBlocks = 4;
+constexpr int kEC = 16;  // doubles per position record of E terms
 
 struct BaWs {
   int4* srec;       // [E]   per position: edge id, ii, jj, kk (clamped to the patch buffer)
   int32_t* poff;    // [E+1] patch -> position range (positions grouped by patch, edges ascending)
-  int32_t* boff;    // [E+1] patch -> pose-block range
-  int32_t* bpose;   // [2E]  free pose of each block (ascending per patch)
+  int32_t* pu;      // [E]   patch of each position
   uint32_t* pmask;  // [E]   free poses touched by each patch
-  int32_t* meta;    // [8]   nuniq, status, nblocks, num_patches, arrival ticket
+  int32_t* meta;    // [8]   nuniq, status, -, num_patches, arrival ticket
   int64_t* kx;      // [E]   unique patch ids (ascending)
-  double* Q;        // [E]
-  double* U;        // [E]
-  double* cb;       // [2E][6]
+  float* J;         // [E][32]  per position: w[2] r[2] Jz[2] Ji[2][6] Jj[2][6]
+  double* EC[2];    // [E][16]  per position: Ei[6] Ej[6] C u (E blocks, ba_cuda.cu:352-373),
+                    //          ii - t0, jj - t0; double-buffered by iteration parity
+  float* dbuf[2];   // [E]      per patch: inverse depth after iteration it (parity it & 1)
   double* S;        // [NL][36]
   double* y;        // [6N]
   double* dX;       // [6N]
+  float* lam;       // [1]   lmbda of the last build (read by the update)
   int64_t* tmark;   // [kMarks]
-  int64_t* wgt;     // [2 x grid] per-workgroup start / end stamps of the last iteration launch
+  int64_t* wgt;     // [2 x grid] per-workgroup start / end stamps of the last Schur launch
 };
 
 struct BaArgs {
@@ -91,27 +92,30 @@ static size_t ba_layout(int E, int N, char* base, BaWs* w) {
   BaWs t;
   t.srec = (int4*)take(sizeof(int4) * E);
   t.poff = (int32_t*)take(sizeof(int32_t) * (E + 1));
-  t.boff = (int32_t*)take(sizeof(int32_t) * (E + 1));
-  t.bpose = (int32_t*)take(sizeof(int32_t) * 2 * E);
+  t.pu = (int32_t*)take(sizeof(int32_t) * E);
   t.pmask = (uint32_t*)take(sizeof(uint32_t) * E);
   t.meta = (int32_t*)take(sizeof(int32_t) * 8);
   t.kx = (int64_t*)take(sizeof(int64_t) * E);
-  t.Q = (double*)take(sizeof(double) * E);
-  t.U = (double*)take(sizeof(double) * E);
-  t.cb = (double*)take(sizeof(double) * 12 * E);
+  t.J = (float*)take(sizeof(float) * 32 * E);
+  t.EC[0] = (double*)take(sizeof(double) * kEC * E);
+  t.EC[1] = (double*)take(sizeof(double) * kEC * E);
+  t.dbuf[0] = (float*)take(sizeof(float) * E);
+  t.dbuf[1] = (float*)take(sizeof(float) * E);
   t.S = (double*)take(sizeof(double) * 36 * (NL ? NL : 1));
   t.y = (double*)take(sizeof(double) * 6 * (N ? N : 1));
   t.dX = (double*)take(sizeof(double) * 6 * (N ? N : 1));
+  t.lam = (float*)take(sizeof(float));
   t.tmark = (int64_t*)take(sizeof(int64_t) * kMarks);
-  t.wgt = (int64_t*)take(sizeof(int64_t) * 2 * (NL + (size_t)E / 256 + 8));
+  t.wgt = (int64_t*)take(sizeof(int64_t) * 2 * (NL + 8));
   if (w) *w = t;
   return off;
 }
 
-// LDS of the iteration kernel: ctl | S lower blocks | rd | y | wave partials
+// LDS of the Schur / solve kernel: ctl | wave partials | solve tail:
+// augmented [6N][6N+1] system, pivot inverse 6x6, column-block snapshot [6N][6]
 static size_t iter_lds(int N) {
-  const size_t NL = (size_t)N * (N + 1) / 2;
-  return kCtlBytes + sizeof(double) * (36 * NL + 12 * (size_t)N + 42 * kIterWaves);
+  const size_t n = 6 * (size_t)N;
+  return kCtlBytes + sizeof(double) * (42 * kIterWaves + n * (n + 1) + 36 + 6 * n);
 }
 
 __device__ __forceinline__ int tri_row(int t) {  // a with a(a+1)/2 <= t < (a+1)(a+2)/2
@@ -267,6 +271,7 @@ __global__ void __launch_bounds__(kSetupThreads) ba_setup_kernel(BaArgs A, BaWs 
         }
         spos[s + 1] = x;
       }
+      for (int t = a; t < b; t++) w.pu[t] = u;
     }
     __syncthreads();
     for (int i = tid; i < E; i += T) {
@@ -340,6 +345,7 @@ __global__ void __launch_bounds__(kSetupThreads) ba_setup_kernel(BaArgs A, BaWs 
 #pragma unroll
     for (int k = 0; k < kPerThread; k++) {
       const int i = tid + k * T;
+      if (i < E) w.pu[i] = work[i] + hd[k] - 1;
       if (i < E && hd[k]) {
         w.kx[work[i]] = kv[k];
         w.poff[work[i]] = i;
@@ -351,11 +357,11 @@ __global__ void __launch_bounds__(kSetupThreads) ba_setup_kernel(BaArgs A, BaWs 
     w.meta[0] = nuniq;
     w.meta[1] = ctl[0] ? 2 : 0;
     w.meta[3] = A.num_patches;
-    w.meta[4] = 0;  // arrival ticket of the iteration kernel
+    w.meta[4] = 0;  // arrival ticket of the Schur kernel
   }
   __syncthreads();
   trace(w.tmark, 41);
-  // per patch: free-pose mask, block count -> block offsets
+  // per patch: free-pose mask
   for (int u = tid; u < nuniq; u += T) {
     unsigned mask = 0;
     for (int t = w.poff[u]; t < w.poff[u + 1]; t++) {
@@ -364,22 +370,6 @@ __global__ void __launch_bounds__(kSetupThreads) ba_setup_kernel(BaArgs A, BaWs 
       if ((c >> 8) != kNoPose) mask |= 1u << (c >> 8);
     }
     w.pmask[u] = mask;
-    work[u] = __popc(mask);
-  }
-  __syncthreads();
-  const int nblocks = block_exclusive_scan(work, nuniq, scr);
-  for (int u = tid; u < nuniq; u += T) {
-    const int base = work[u];
-    const unsigned mask = w.pmask[u];
-    w.boff[u] = base;
-    for (unsigned m = mask; m; m &= m - 1) {
-      const int p = __ffs(m) - 1;
-      w.bpose[base + __popc(mask & ((1u << p) - 1u))] = p;
-    }
-  }
-  if (tid == 0) {
-    w.boff[nuniq] = nblocks;
-    w.meta[2] = nblocks;
   }
   trace(w.tmark, 42);
 }
@@ -388,7 +378,7 @@ __global__ void __launch_bounds__(kSetupThreads) ba_setup_kernel(BaArgs A, BaWs 
 __device__ __forceinline__ void edge_linearize(const float* poses, const float* patches, int P,
                                                float fx, float fy, float cx, float cy, float tx,
                                                float ty, float wx, float wy, int ix, int jx,
-                                               int64_t kx, float* o) {
+                                               int64_t kx, bool use_depth, float depth, float* o) {
   const float* pi = poses + 7 * (size_t)ix;
   const float* pj = poses + 7 * (size_t)jx;
   const float* pk = patches + (size_t)kx * 3 * P * P;
@@ -399,7 +389,7 @@ __device__ __forceinline__ void edge_linearize(const float* poses, const float* 
   Xi[0] = (pk[c11] - cx) / fx;
   Xi[1] = (pk[P * P + c11] - cy) / fy;
   Xi[2] = 1.0f;
-  Xi[3] = pk[2 * P * P + c11];
+  Xi[3] = use_depth ? depth : pk[2 * P * P + c11];
   float tij[3], qij[4];
   relSE3(ti, qi, tj, qj, tij, qij);
   actSE3(tij, qij, Xi, Xj);
@@ -468,76 +458,173 @@ __global__ void reproject_kernel(const float* __restrict__ poses, const float* _
 #pragma clang fp contract(fast)
 
 // ---------------------------------------------------------------------------
-// Per-patch linearisation shared by the Schur-block and patch-owner
-// workgroups: all edges of patch u (positions [poff[u], poff[u+1])).
+// Inverse-depth retraction of patch u (dZ = Q (u - E^T dX), ba_cuda.cu:563;
+// patch_retr_kernel :209-229) from the E terms of the iteration that
+// produced dX, applied to `base` (the depth that iteration used).
 // ---------------------------------------------------------------------------
-struct Intr {
-  float fx, fy, cx, cy;
-};
+__device__ __forceinline__ float retract_depth(const BaWs& w, const double* EC, const double* dX,
+                                               int t0, int N, double lam, int u, float base) {
+  double C = 0.0, Uu = 0.0, ex = 0.0;  // ex = (E^T dX)_u
+  const int p1 = w.poff[u + 1];
+#pragma unroll 2
+  for (int t = w.poff[u]; t < p1; t++) {
+    const double* ec = EC + kEC * (size_t)t;
+    const int pi = (int)ec[14], pj = (int)ec[15];
+    C += ec[12];
+    Uu += ec[13];
+    if (pi >= 0 && pi < N)
+#pragma unroll
+      for (int k = 0; k < 6; k++) ex += ec[k] * dX[6 * pi + k];
+    if (pj >= 0 && pj < N)
+#pragma unroll
+      for (int k = 0; k < 6; k++) ex += ec[6 + k] * dX[6 * pj + k];
+  }
+  const float dz = (float)((1.0 / (C + lam)) * (Uu - ex));  // Q = 1/(C + lmbda) (:519)
+  float d = base + dz;
+  d = (d > 20.0f) ? 1.0f : d;
+  return (float)fmax((double)d, 1e-4);
+}
 
-// edge at position t -> o[30] (w r Jz Ji Jj), pi/pj free-pose indices
-__device__ __forceinline__ void linearize_position(const BaArgs& A, const int4* __restrict__ srec,
-                                                   const Intr& K, int kmax, int t, float* o,
-                                                   int& pi, int& pj) {
-  const int4 r = srec[t];
+// ---------------------------------------------------------------------------
+// LINEARIZE (ba_lin_kernel, iteration `it`): thread per position.  For
+// it > 0 the thread first retracts its patch's depth with the previous
+// iteration's dX (every thread of a patch computes the same value; the
+// patch's first position records it), then runs the fp32 edge math of the
+// reference at that depth -> J, and the edge's E/C/u terms in fp64 -> EC.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) ba_lin_kernel(BaArgs A, BaWs w, int it) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) w.lam[0] = A.lmbda[0];
+  if (t >= A.E) return;
+  const float fx = A.intrinsics[0], fy = A.intrinsics[1], cx = A.intrinsics[2],
+              cy = A.intrinsics[3];
+  const int4 r = w.srec[t];
+  const int kmax = w.meta[3] - 1;
+  float depth = 0.0f;
+  if (it > 0) {
+    const int u = w.pu[t], P = A.P;
+    const float base = (it == 1)
+                           ? A.patches[(size_t)min(r.w, kmax) * 3 * P * P + 2 * P * P]
+                           : w.dbuf[(it - 1) & 1][u];
+    depth = retract_depth(w, w.EC[(it - 1) & 1], w.dX, A.t0, A.N, (double)A.lmbda[0], u, base);
+    if (t == w.poff[u]) w.dbuf[it & 1][u] = depth;
+  }
   const float2 tg = reinterpret_cast<const float2*>(A.target)[r.x];
   const float2 wt = reinterpret_cast<const float2*>(A.weight)[r.x];
   const int ix = min(max(r.y, 0), A.num_poses - 1);  // memory guard (reference: unchecked)
   const int jx = min(max(r.z, 0), A.num_poses - 1);
-  edge_linearize(A.poses, A.patches, A.P, K.fx, K.fy, K.cx, K.cy, tg.x, tg.y, wt.x, wt.y, ix, jx,
-                 (int64_t)min(r.w, kmax), o);
-  pi = r.y - A.t0;
-  pj = r.z - A.t0;
+  float o[30];
+  edge_linearize(A.poses, A.patches, A.P, fx, fy, cx, cy, tg.x, tg.y, wt.x, wt.y, ix, jx,
+                 (int64_t)min(r.w, kmax), it > 0, depth, o);
+  float4* Jo = reinterpret_cast<float4*>(w.J + 32 * (size_t)t);
+#pragma unroll
+  for (int k = 0; k < 7; k++) Jo[k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+  reinterpret_cast<float2*>(Jo + 7)[0] = make_float2(o[28], o[29]);
+  double ec[kEC];
+#pragma unroll
+  for (int k = 0; k < 14; k++) ec[k] = 0.0;
+#pragma unroll
+  for (int row = 0; row < 2; row++) {  // ba_cuda.cu:352-373
+    const double wr = o[row];
+    const float rr = o[2 + row], Jz = o[4 + row];
+    const double wz = wr * Jz;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      ec[k] -= wz * o[6 + 6 * row + k];
+      ec[6 + k] += wz * o[18 + 6 * row + k];
+    }
+    ec[12] += wz * Jz;
+    ec[13] += wr * rr * Jz;
+  }
+  ec[14] = (double)(r.y - A.t0);  // pose codes: free iff in [0, N)
+  ec[15] = (double)(r.z - A.t0);
+  double2* Eo = reinterpret_cast<double2*>(w.EC[it & 1] + kEC * (size_t)t);
+#pragma unroll
+  for (int k = 0; k < kEC / 2; k++) Eo[k] = make_double2(ec[2 * k], ec[2 * k + 1]);
 }
 
-// Schur block (a, b), a >= b, contributions of patch u, accumulated into
-// acc[36] (row-major 6x6) and yv[6] (diagonal blocks only).
-__device__ __forceinline__ void patch_schur_terms(const BaArgs& A, const BaWs& w, const Intr& K,
-                                                  int kmax, double lam, int u, int a, int b,
-                                                  double* acc, double* yv) {
+// After the last iteration (`iters` of them): write every patch's final
+// inverse depth to all P x P entries (patch_retr_kernel :225-228).
+__global__ void __launch_bounds__(256) ba_apply_kernel(BaArgs A, BaWs w, int iters) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= w.meta[0]) return;
+  const int P = A.P, last = iters - 1;
+  float* pk = A.patches + (size_t)w.kx[u] * 3 * P * P + 2 * P * P;
+  const float base = (last == 0) ? pk[0] : w.dbuf[last & 1][u];
+  const float d = retract_depth(w, w.EC[last & 1], w.dX, A.t0, A.N, (double)w.lam[0], u, base);
+  for (int k = 0; k < P * P; k++) pk[k] = d;
+}
+
+// ---------------------------------------------------------------------------
+// SCHUR block (a, b), a >= b: patch u's terms, gathered from J / EC.
+// acc[0..36): row-major 6x6 block, acc[36..42): y_a (diagonal blocks).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void patch_schur_terms(const BaWs& w, const double* EC, int t0,
+                                                  double lam, int u, int a, int b, double* acc) {
   const bool diag = a == b;
   double C = 0.0, Uu = 0.0, ca[6], cc[6];
 #pragma unroll
   for (int k = 0; k < 6; k++) ca[k] = cc[k] = 0.0;
-  const int t1 = w.poff[u + 1];
-  for (int t = w.poff[u]; t < t1; t++) {
-    float o[30];
-    int pi, pj;
-    linearize_position(A, w.srec, K, kmax, t, o, pi, pj);
+  const int p1 = w.poff[u + 1];
+#pragma unroll 2
+  for (int t = w.poff[u]; t < p1; t++) {
+    const double2* ep = reinterpret_cast<const double2*>(EC + kEC * (size_t)t);
+    double ec[kEC];
+#pragma unroll
+    for (int k = 0; k < kEC / 2; k++) {
+      const double2 v = ep[k];
+      ec[2 * k] = v.x;
+      ec[2 * k + 1] = v.y;
+    }
+    const int pi = (int)ec[14], pj = (int)ec[15];
+    C += ec[12];
+    Uu += ec[13];
+    if (pi == a)
+#pragma unroll
+      for (int k = 0; k < 6; k++) ca[k] += ec[k];
+    if (pj == a)
+#pragma unroll
+      for (int k = 0; k < 6; k++) ca[k] += ec[6 + k];
+    if (!diag) {
+      if (pi == b)
+#pragma unroll
+        for (int k = 0; k < 6; k++) cc[k] += ec[k];
+      if (pj == b)
+#pragma unroll
+        for (int k = 0; k < 6; k++) cc[k] += ec[6 + k];
+    }
+    // B and v (ba_cuda.cu:339-370): only edges whose poses are (a, a) / {a, b}
+    const bool inB = diag ? (pi == a || pj == a) : ((pi == a && pj == b) || (pi == b && pj == a));
+    if (!inB) continue;
+    const float4* J4 = reinterpret_cast<const float4*>(w.J + 32 * (size_t)t);
+    float o[32];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const float4 v = J4[k];
+      o[4 * k] = v.x;
+      o[4 * k + 1] = v.y;
+      o[4 * k + 2] = v.z;
+      o[4 * k + 3] = v.w;
+    }
+    const bool rows_i = (pi == a);  // off-diagonal: rows follow pose a
 #pragma unroll
     for (int row = 0; row < 2; row++) {
       const double wr = o[row];
-      const float r = o[2 + row], Jz = o[4 + row];
-      const float* Ji = o + 6 + 6 * row;
-      const float* Jj = o + 18 + 6 * row;
-      const double wz = wr * Jz;
-      C += wz * Jz;  // ba_cuda.cu:372-373
-      Uu += wr * r * Jz;
-      // E column blocks of poses a (and b) (:352-363)
-      if (pi == a)
+      const double wrr = wr * o[2 + row];
+      float Ji[6], Jj[6];
 #pragma unroll
-        for (int k = 0; k < 6; k++) ca[k] -= wz * Ji[k];
-      if (pj == a)
-#pragma unroll
-        for (int k = 0; k < 6; k++) ca[k] += wz * Jj[k];
-      if (!diag) {
-        if (pi == b)
-#pragma unroll
-          for (int k = 0; k < 6; k++) cc[k] -= wz * Ji[k];
-        if (pj == b)
-#pragma unroll
-          for (int k = 0; k < 6; k++) cc[k] += wz * Jj[k];
+      for (int k = 0; k < 6; k++) {
+        Ji[k] = o[6 + 6 * row + k];
+        Jj[k] = o[18 + 6 * row + k];
       }
-      // B and v (:339-370)
       if (diag) {
-        const double wrr = wr * r;
         if (pi == a) {
 #pragma unroll
           for (int x = 0; x < 6; x++) {
             const double wx = wr * Ji[x];
 #pragma unroll
             for (int z = 0; z < 6; z++) acc[6 * x + z] += wx * Ji[z];
-            yv[x] -= wrr * Ji[x];
+            acc[36 + x] -= wrr * Ji[x];
           }
         }
         if (pj == a) {
@@ -546,7 +633,7 @@ __device__ __forceinline__ void patch_schur_terms(const BaArgs& A, const BaWs& w
             const double wx = wr * Jj[x];
 #pragma unroll
             for (int z = 0; z < 6; z++) acc[6 * x + z] += wx * Jj[z];
-            yv[x] += wrr * Jj[x];
+            acc[36 + x] += wrr * Jj[x];
           }
         }
         if (pi == a && pj == a) {
@@ -556,101 +643,29 @@ __device__ __forceinline__ void patch_schur_terms(const BaArgs& A, const BaWs& w
             for (int z = 0; z < 6; z++) acc[6 * x + z] -= wr * Ji[x] * Jj[z] + wr * Jj[x] * Ji[z];
         }
       } else {
-        if (pi == a && pj == b) {
+        // rows follow pose a: Ji when ii == a, Jj when jj == a
 #pragma unroll
-          for (int x = 0; x < 6; x++) {
-            const double wx = wr * Ji[x];
+        for (int x = 0; x < 6; x++) {
+          const double wx = wr * (rows_i ? Ji[x] : Jj[x]);
 #pragma unroll
-            for (int z = 0; z < 6; z++) acc[6 * x + z] -= wx * Jj[z];
-          }
-        }
-        if (pj == a && pi == b) {
-#pragma unroll
-          for (int x = 0; x < 6; x++) {
-            const double wx = wr * Jj[x];
-#pragma unroll
-            for (int z = 0; z < 6; z++) acc[6 * x + z] -= wx * Ji[z];
-          }
+          for (int z = 0; z < 6; z++) acc[6 * x + z] -= wx * (rows_i ? Jj[z] : Ji[z]);
         }
       }
     }
   }
   // - E Q E^T and - E Q u (:554-558)
-  const double q = 1.0 / (C + lam);
-  const double* cb = diag ? ca : cc;
+  const double q = 1.0 / (C + lam);  // :519
+  const double* cr = diag ? ca : cc;
 #pragma unroll
   for (int x = 0; x < 6; x++) {
     const double cq = ca[x] * q;
 #pragma unroll
-    for (int z = 0; z < 6; z++) acc[6 * x + z] -= cq * cb[z];
+    for (int z = 0; z < 6; z++) acc[6 * x + z] -= cq * cr[z];
   }
   if (diag) {
     const double qu = q * Uu;
 #pragma unroll
-    for (int x = 0; x < 6; x++) yv[x] -= ca[x] * qu;
-  }
-}
-
-// Q_u, U_u and every c_{u,p} of patch u (patch-owner workgroups)
-__device__ __forceinline__ void patch_owner_terms(const BaArgs& A, const BaWs& w, const Intr& K,
-                                                  int kmax, double lam, int u) {
-  const int s0 = w.boff[u], nb = w.boff[u + 1] - s0;
-  const unsigned mask = w.pmask[u];
-  double C = 0.0, Uu = 0.0, c[kRegBlocks][6];
-#pragma unroll
-  for (int s = 0; s < kRegBlocks; s++)
-#pragma unroll
-    for (int k = 0; k < 6; k++) c[s][k] = 0.0;
-  const int t1 = w.poff[u + 1];
-  for (int t = w.poff[u]; t < t1; t++) {
-    float o[30];
-    int pi, pj;
-    linearize_position(A, w.srec, K, kmax, t, o, pi, pj);
-    const bool fi = pi >= 0 && pi < A.N, fj = pj >= 0 && pj < A.N;
-    const int si = fi ? __popc(mask & ((1u << pi) - 1u)) : -1;
-    const int sj = fj ? __popc(mask & ((1u << pj) - 1u)) : -1;
-#pragma unroll
-    for (int row = 0; row < 2; row++) {
-      const double wr = o[row];
-      const float r = o[2 + row], Jz = o[4 + row];
-      const double wz = wr * Jz;
-      C += wz * Jz;
-      Uu += wr * r * Jz;
-      if (nb <= kRegBlocks) {
-#pragma unroll
-        for (int s = 0; s < kRegBlocks; s++) {
-          if (si == s)
-#pragma unroll
-            for (int k = 0; k < 6; k++) c[s][k] -= wz * o[6 + 6 * row + k];
-          if (sj == s)
-#pragma unroll
-            for (int k = 0; k < 6; k++) c[s][k] += wz * o[18 + 6 * row + k];
-        }
-      } else {  // rare: many poses on one patch -> accumulate in place
-        double* cs = w.cb + 6 * (size_t)s0;
-        if (t == w.poff[u] && row == 0)
-          for (int k = 0; k < 6 * nb; k++) cs[k] = 0.0;
-        if (si >= 0)
-#pragma unroll
-          for (int k = 0; k < 6; k++) cs[6 * si + k] -= wz * o[6 + 6 * row + k];
-        if (sj >= 0)
-#pragma unroll
-          for (int k = 0; k < 6; k++) cs[6 * sj + k] += wz * o[18 + 6 * row + k];
-      }
-    }
-  }
-  w.Q[u] = 1.0 / (C + lam);  // ba_cuda.cu:519
-  w.U[u] = Uu;
-  if (nb <= kRegBlocks) {
-#pragma unroll
-    for (int s = 0; s < kRegBlocks; s++) {
-      if (s < nb) {
-        double2* co = reinterpret_cast<double2*>(w.cb + 6 * (size_t)(s0 + s));
-        co[0] = make_double2(c[s][0], c[s][1]);
-        co[1] = make_double2(c[s][2], c[s][3]);
-        co[2] = make_double2(c[s][4], c[s][5]);
-      }
-    }
+    for (int x = 0; x < 6; x++) acc[36 + x] -= ca[x] * qu;
   }
 }
 
@@ -675,205 +690,188 @@ __device__ __forceinline__ double wave_sum_to_63(double v) {
   return v;
 }
 
-// sum of NV per-thread values over the workgroup, in a fixed order; the
-// result lands in red[0..NV) (LDS).  part: kIterWaves * NV doubles of LDS.
+// sum of NV per-thread values over the workgroup in a fixed order -> red[]
+// (LDS).  Only waves below `active_waves` hold non-zero values (the
+// compacted patch list fills threads from 0); the others skip the DPP tree.
+// part: (blockDim/64) * NV doubles of LDS.
 template <int NV>
-__device__ __forceinline__ void block_sum(const double* v, double* part, double* red) {
+__device__ __forceinline__ void block_sum(const double* v, double* part, double* red,
+                                          int active_waves) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = min((int)(blockDim.x >> 6), max(active_waves, 1));
+  if (wid < nw) {
 #pragma unroll
-  for (int i = 0; i < NV; i++) {
-    const double s = wave_sum_to_63(v[i]);
-    if (lane == 63) part[wid * NV + i] = s;
+    for (int i = 0; i < NV; i++) {
+      const double s = wave_sum_to_63(v[i]);
+      if (lane == 63) part[wid * NV + i] = s;
+    }
   }
   __syncthreads();
   if (threadIdx.x < NV) {
     double s = 0.0;
-    for (int k = 0; k < (int)(blockDim.x >> 6); k++) s += part[k * NV + threadIdx.x];
+    for (int k = 0; k < nw; k++) s += part[k * NV + threadIdx.x];
     red[threadIdx.x] = s;
   }
   __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
-// SOLVE tail (one workgroup): damped S (lower blocks in LDS) -> L in place,
-// y -> dX in place; rd[6k + c] = 1 / L_kk[c][c].
+// SOLVE tail: damped S x = y by block Gauss-Jordan (6x6 pivot blocks) on the
+// augmented system in LDS -- SPD, no pivoting needed; the elimination of
+// every row block at each step folds the back substitution in, so the
+// critical path is one 6x6 inversion per pose.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double rsqrt_d(double x) {  // estimate + one Newton step
-  const double r = __builtin_amdgcn_rsq(x);
-  return r * (1.5 - (0.5 * x) * r * r);
+__device__ __forceinline__ double rcp_d(double x) {  // estimate + one Newton step
+  const double r = __builtin_amdgcn_rcp(x);
+  return __builtin_fma(r, __builtin_fma(-x, r, 1.0), r);
 }
 
-// one lane: Cholesky of a 6x6 pivot block held in registers
-__device__ __forceinline__ bool factor_block_lane(double* Sb, double* rd) {
-  double L[6][6];
+// one lane: in-place Gauss-Jordan inverse of an SPD 6x6 block (registers)
+__device__ __forceinline__ bool invert6(const double* M, int ld, double* Pinv) {
+  double a[6][6];
 #pragma unroll
   for (int r = 0; r < 6; r++)
 #pragma unroll
-    for (int c = 0; c <= r; c++) L[r][c] = Sb[6 * r + c];
+    for (int c = 0; c < 6; c++) a[r][c] = M[r * ld + c];
   bool ok = true;
 #pragma unroll
   for (int c = 0; c < 6; c++) {
-    const double d = L[c][c];
-    ok = ok && (d > 0.0);
-    const double rs = rsqrt_d(d);
-    rd[c] = rs;
-    L[c][c] = d * rs;
+    const double piv = a[c][c];
+    ok = ok && (piv > 0.0);
+    const double r = rcp_d(piv);
+    a[c][c] = 1.0;
 #pragma unroll
-    for (int r = c + 1; r < 6; r++) L[r][c] *= rs;
+    for (int j = 0; j < 6; j++) a[c][j] *= r;
 #pragma unroll
-    for (int c2 = c + 1; c2 < 6; c2++)
+    for (int i = 0; i < 6; i++) {
+      if (i == c) continue;
+      const double f = a[i][c];
+      a[i][c] = 0.0;
 #pragma unroll
-      for (int r = c2; r < 6; r++) L[r][c2] -= L[r][c] * L[c2][c];
+      for (int j = 0; j < 6; j++) a[i][j] -= f * a[c][j];
+    }
   }
 #pragma unroll
   for (int r = 0; r < 6; r++)
 #pragma unroll
-    for (int c = 0; c < 6; c++) Sb[6 * r + c] = c <= r ? L[r][c] : 0.0;
+    for (int c = 0; c < 6; c++) Pinv[6 * r + c] = a[r][c];
   return ok;
 }
 
-// row r of block (a, b) -= row r of L_ak times L_bk^T
-__device__ __forceinline__ void trailing_row(double* S, int k, int a, int b, int r) {
-  const double* la = S + 36 * blk(a, k) + 6 * r;
-  const double* lb = S + 36 * blk(b, k);
-  double* row = S + 36 * blk(a, b) + 6 * r;
-  double lr[6];
-#pragma unroll
-  for (int q = 0; q < 6; q++) lr[q] = la[q];
-#pragma unroll
-  for (int c = 0; c < 6; c++) {
-    double v = row[c];
-#pragma unroll
-    for (int q = 0; q < 6; q++) v -= lr[q] * lb[6 * c + q];
-    row[c] = v;
-  }
+struct TailLds {
+  int* ctl;      // [0] last-arrival flag, [1] failure
+  double* part;  // kIterWaves x 42
+  double* M;     // [n][n+1] augmented system
+  double* Pinv;  // [36]
+  double* Cb;    // [n][6] snapshot of the pivot column block
+};
+__device__ __forceinline__ TailLds tail_carve(char* lds, int N) {
+  const int n = 6 * N;
+  TailLds s;
+  s.ctl = reinterpret_cast<int*>(lds);
+  s.part = reinterpret_cast<double*>(lds + kCtlBytes);
+  s.M = s.part + 42 * kIterWaves;
+  s.Pinv = s.M + (size_t)n * (n + 1);
+  s.Cb = s.Pinv + 36;
+  return s;
 }
 
-__device__ void ba_solve(int N, double* S, double* rd, double* y, int* fail, int64_t* tr) {
-  const int tid = threadIdx.x, T = blockDim.x, wid = tid >> 6, lane = tid & 63;
-  for (int t = tid; t < 6 * N; t += T) {  // S += I * (1e-4 S + 1)  (ba_cuda.cu:560)
-    double* d = S + 36 * blk(t / 6, t / 6) + 7 * (t % 6);
-    *d += 1e-4 * *d + 1.0;
-  }
-  __syncthreads();
-  if (tid == 0) *fail = factor_block_lane(S, rd) ? 0 : 1;
+// x overwrites column n of M; returns failure
+__device__ int ba_solve_gj(int N, const TailLds& L, int64_t* tr) {
+  const int tid = threadIdx.x, T = blockDim.x, n = 6 * N, ld = n + 1;
+  double* M = L.M;
+  if (tid == 0) L.ctl[1] = invert6(M, ld, L.Pinv) ? 0 : 1;
   __syncthreads();
   trace(tr, 50);
   for (int k = 0; k < N; k++) {
-    const int m = N - k - 1;
-    {  // panel: L_ak = S_ak L_kk^{-T}, right-looking substitution per row
-      const double* Lkk = S + 36 * blk(k, k);
-      double lk[6][6], rk[6];
+    const int k0 = 6 * k, c0 = k0 + 6;  // columns left of c0 are already eliminated
+    // (1) pivot rows: row block k <- Pinv * row block k (columns c0..n);
+    //     snapshot the pivot column block of the other rows
+    for (int c = c0 + tid; c <= n; c += T) {
+      double v[6], o[6];
 #pragma unroll
-      for (int c = 0; c < 6; c++) {
-        rk[c] = rd[6 * k + c];
+      for (int q = 0; q < 6; q++) v[q] = M[(k0 + q) * ld + c];
 #pragma unroll
-        for (int q = 0; q < c; q++) lk[c][q] = Lkk[6 * c + q];
+      for (int r = 0; r < 6; r++) {
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < 6; q++) s += L.Pinv[6 * r + q] * v[q];
+        o[r] = s;
       }
-      for (int t = tid; t < 6 * m; t += T) {
-        const int a = k + 1 + t / 6, r = t % 6;
-        double* row = S + 36 * blk(a, k) + 6 * r;
-        double x[6];
 #pragma unroll
-        for (int c = 0; c < 6; c++) x[c] = row[c];
-#pragma unroll
-        for (int c = 0; c < 6; c++) {
-          x[c] *= rk[c];
-#pragma unroll
-          for (int c2 = c + 1; c2 < 6; c2++) x[c2] -= x[c] * lk[c2][c];
-        }
-#pragma unroll
-        for (int c = 0; c < 6; c++) row[c] = x[c];
-      }
+      for (int r = 0; r < 6; r++) M[(k0 + r) * ld + c] = o[r];
     }
+    for (int t = tid; t < 6 * n; t += T) L.Cb[t] = M[(t / 6) * ld + k0 + t % 6];
     __syncthreads();
-    if (m == 0) break;
-    // trailing update; wave 0 takes block (k+1, k+1) and factors it right
-    // away (look-ahead) while the other waves update the rest
-    if (wid == 0) {
-      if (lane < 6) trailing_row(S, k, k + 1, k + 1, lane);
+    trace(tr, 60 + 2 * k);
+    // (2) eliminate the pivot column block from every other row.  Wave 0
+    //     first updates the next pivot block (k+1, k+1) and inverts it
+    //     (look-ahead) while the other waves eliminate everything else: a
+    //     thread owns one column and a strided group of rows, 4 rows per
+    //     batch of independent loads.
+    const int ncol = n + 1 - c0, nrow = n - 6;
+    const bool ahead = (k + 1 < N);
+    if (ahead && tid < 64) {
+      if (tid < 36) {
+        const int r = c0 + tid / 6, c = c0 + tid % 6;
+        const double* f = L.Cb + 6 * r;
+        double v = M[r * ld + c];
+#pragma unroll
+        for (int q = 0; q < 6; q++) v -= f[q] * M[(k0 + q) * ld + c];
+        M[r * ld + c] = v;
+      }
       wave_lds_sync();
-      if (lane == 0 && !factor_block_lane(S + 36 * blk(k + 1, k + 1), rd + 6 * (k + 1))) *fail = 1;
-    } else {
-      const int ntask = 6 * (m * (m + 1) / 2 - 1);
-      for (int t = tid - 64; t < ntask; t += T - 64) {
-        const int j = 1 + t / 6, r = t % 6;
-        const int ap = tri_row(j), bp = j - ap * (ap + 1) / 2;
-        trailing_row(S, k, k + 1 + ap, k + 1 + bp, r);
+      if (tid == 0 && !invert6(M + (size_t)c0 * ld + c0, ld, L.Pinv)) L.ctl[1] = 1;
+    }
+    const int T2 = ahead ? T - 64 : T, tid2 = ahead ? tid - 64 : tid;
+    const int G = max(1, min(nrow, T2 / ncol));
+    if (tid2 >= 0) {
+      for (int task = tid2; task < ncol * G; task += T2) {
+        const int c = c0 + task % ncol, g = task / ncol;
+        double tq[6];
+#pragma unroll
+        for (int q = 0; q < 6; q++) tq[q] = M[(k0 + q) * ld + c];
+        for (int i0 = g; i0 < nrow; i0 += 4 * G) {
+          int rows[4];
+          double v[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const int i = i0 + j * G;
+            rows[j] = (i < nrow) ? i + ((i >= k0) ? 6 : 0) : -1;
+            // the look-ahead block was already updated by wave 0
+            if (ahead && rows[j] >= c0 && rows[j] < c0 + 6 && c < c0 + 6) rows[j] = -1;
+            v[j] = rows[j] >= 0 ? M[rows[j] * ld + c] : 0.0;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            if (rows[j] < 0) continue;
+            const double* f = L.Cb + 6 * rows[j];
+            double x = v[j];
+#pragma unroll
+            for (int q = 0; q < 6; q++) x -= f[q] * tq[q];
+            M[rows[j] * ld + c] = x;
+          }
+        }
       }
     }
     __syncthreads();
+    trace(tr, 61 + 2 * k);
   }
   trace(tr, 51);
-  if (*fail) {
-    for (int t = tid; t < 6 * N; t += T) y[t] = 0.0;  // dX = 0 (dpvo/ba.py:17-21)
-  } else if (wid == 0) {
-    // forward: z_k = L_kk^{-1} y_k, then y_a -= L_ak z_k (a > k)
-    for (int k = 0; k < N; k++) {
-      const double* Lkk = S + 36 * blk(k, k);
-      double z[6];
-#pragma unroll
-      for (int c = 0; c < 6; c++) z[c] = y[6 * k + c];
-#pragma unroll
-      for (int c = 0; c < 6; c++) {
-        z[c] *= rd[6 * k + c];
-#pragma unroll
-        for (int c2 = c + 1; c2 < 6; c2++) z[c2] -= z[c] * Lkk[6 * c2 + c];
-      }
-      for (int t = lane; t < 6 * (N - k - 1); t += 64) {
-        const int a = k + 1 + t / 6, r = t % 6;
-        const double* la = S + 36 * blk(a, k) + 6 * r;
-        double v = y[6 * a + r];
-#pragma unroll
-        for (int c = 0; c < 6; c++) v -= la[c] * z[c];
-        y[6 * a + r] = v;
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int r = 0; r < 6; r++)
-        if (lane == r) y[6 * k + r] = z[r];
-      wave_lds_sync();
-    }
-    // backward: x_k = L_kk^{-T} z_k, then z_b -= L_kb^T x_k (b < k)
-    for (int k = N - 1; k >= 0; k--) {
-      const double* Lkk = S + 36 * blk(k, k);
-      double x[6];
-#pragma unroll
-      for (int c = 0; c < 6; c++) x[c] = y[6 * k + c];
-#pragma unroll
-      for (int c = 5; c >= 0; c--) {
-        x[c] *= rd[6 * k + c];
-#pragma unroll
-        for (int c2 = 0; c2 < c; c2++) x[c2] -= x[c] * Lkk[6 * c + c2];
-      }
-      for (int t = lane; t < 6 * k; t += 64) {
-        const int b = t / 6, r = t % 6;
-        const double* lk = S + 36 * blk(k, b);
-        double v = y[6 * b + r];
-#pragma unroll
-        for (int c = 0; c < 6; c++) v -= lk[6 * c + r] * x[c];
-        y[6 * b + r] = v;
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int r = 0; r < 6; r++)
-        if (lane == r) y[6 * k + r] = x[r];
-      wave_lds_sync();
-    }
-  }
-  __syncthreads();
-  trace(tr, 52);
+  return L.ctl[1];
 }
 
 // ---------------------------------------------------------------------------
-// UPDATE: pose_retr_kernel (:178-206), dZ (:563), patch_retr_kernel (:209-229)
+// POSE UPDATE: dX out, pose_retr_kernel (:178-206).  x: dX (6N, stride xs).
+// The patch retraction happens in the next ba_lin_kernel / ba_apply_kernel.
 // ---------------------------------------------------------------------------
-__device__ void ba_update(const BaArgs& A, const BaWs& w, const double* x, int fail,
-                          double* dX_out) {
+__device__ void ba_pose_update(const BaArgs& A, const BaWs& w, const double* x, int xs, int fail,
+                               double* dX_out) {
   const int tid = threadIdx.x, T = blockDim.x, N = A.N;
   for (int i = tid; i < 6 * N; i += T) {
-    w.dX[i] = x[i];
-    if (dX_out) dX_out[i] = x[i];
+    const double v = fail ? 0.0 : x[i * xs];  // failed factorisation: dX = 0 (dpvo/ba.py:17-21)
+    w.dX[i] = v;
+    if (dX_out) dX_out[i] = v;
   }
   if (tid == 0) w.meta[1] = (w.meta[1] & ~1) | (fail ? 1 : 0);
   for (int i = tid; i < N; i += T) {
@@ -882,97 +880,111 @@ __device__ void ba_update(const BaArgs& A, const BaWs& w, const double* x, int f
     float* pt = A.poses + 7 * (size_t)t;
     float xi[6], t1[3], q1[4];
 #pragma unroll
-    for (int k = 0; k < 6; k++) xi[k] = (float)x[6 * i + k];
+    for (int k = 0; k < 6; k++) xi[k] = fail ? 0.0f : (float)x[(6 * i + k) * xs];
     float tt[3] = {pt[0], pt[1], pt[2]}, qq[4] = {pt[3], pt[4], pt[5], pt[6]};
     retrSE3(xi, tt, qq, t1, q1);
     pt[0] = t1[0]; pt[1] = t1[1]; pt[2] = t1[2];
     pt[3] = q1[0]; pt[4] = q1[1]; pt[5] = q1[2]; pt[6] = q1[3];
   }
-  const int nuniq = w.meta[0], P = A.P;
-  for (int u = tid; u < nuniq; u += T) {
-    double s = w.U[u];
-    for (int b = w.boff[u]; b < w.boff[u + 1]; b++) {
-      const double2* c = reinterpret_cast<const double2*>(w.cb + 6 * (size_t)b);
-      const double2 c01 = c[0], c23 = c[1], c45 = c[2];
-      const double* xp = x + 6 * w.bpose[b];
-      s -= c01.x * xp[0];
-      s -= c01.y * xp[1];
-      s -= c23.x * xp[2];
-      s -= c23.y * xp[3];
-      s -= c45.x * xp[4];
-      s -= c45.y * xp[5];
-    }
-    const float dz = (float)(w.Q[u] * s);
-    float* pk = A.patches + (size_t)w.kx[u] * 3 * P * P + 2 * P * P;
-    float d = pk[0] + dz;
-    d = (d > 20.0f) ? 1.0f : d;
-    d = (float)fmax((double)d, 1e-4);
-    for (int k = 0; k < P * P; k++) pk[k] = d;
-  }
 }
 
-struct IterLds {
-  int* ctl;  // [0] last-arrival flag, [1] Cholesky failure
-  double* S;
-  double* rd;
-  double* y;
-  double* part;  // kIterWaves x 42
-};
-__device__ __forceinline__ IterLds iter_carve(char* lds, int N) {
-  IterLds s;
-  s.ctl = reinterpret_cast<int*>(lds);
-  s.S = reinterpret_cast<double*>(lds + kCtlBytes);
-  s.rd = s.S + 36 * (N * (N + 1) / 2);
-  s.y = s.rd + 6 * N;
-  s.part = s.y + 6 * N;
-  return s;
-}
-
-// the solve tail: S, y from global -> LDS, factor, substitute, update
+// the solve tail: S (lower blocks), y from global -> augmented system in
+// LDS, damping, Gauss-Jordan, update
 __device__ void ba_solve_tail(const BaArgs& A, const BaWs& w, const double* S_in,
-                              const double* y_in, double* dX_out, const IterLds& L, int64_t* tr) {
-  const int N = A.N, NL = N * (N + 1) / 2;
+                              const double* y_in, double* dX_out, const TailLds& L, int64_t* tr) {
+  const int N = A.N, n = 6 * N, ld = n + 1;
   int fail = 0;
   if (N > 0) {
-    for (int t = threadIdx.x; t < 36 * NL; t += blockDim.x) L.S[t] = S_in[t];
-    for (int t = threadIdx.x; t < 6 * N; t += blockDim.x) L.y[t] = y_in[t];
+    // batches of 16 independent loads per thread (one latency per batch)
+    constexpr int B = 16;
+    for (int t0 = threadIdx.x; t0 < n * n; t0 += B * blockDim.x) {
+      double v[B];
+#pragma unroll
+      for (int j = 0; j < B; j++) {
+        const int t = t0 + j * blockDim.x;
+        v[j] = 0.0;
+        if (t < n * n) {
+          const int r = t / n, c = t % n, ar = r / 6, ac = c / 6;
+          // lower blocks hold (a, b), a >= b; the upper half is the transpose
+          v[j] = (ar >= ac) ? S_in[36 * blk(ar, ac) + 6 * (r % 6) + c % 6]
+                            : S_in[36 * blk(ac, ar) + 6 * (c % 6) + r % 6];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < B; j++) {
+        const int t = t0 + j * blockDim.x;
+        if (t < n * n) {
+          const int r = t / n, c = t % n;
+          double x = v[j];
+          if (r == c) x += 1e-4 * x + 1.0;  // S += I * (1e-4 S + 1)  (ba_cuda.cu:560)
+          L.M[r * ld + c] = x;
+        }
+      }
+    }
+    for (int r = threadIdx.x; r < n; r += blockDim.x) L.M[r * ld + n] = y_in[r];
     __syncthreads();
-    ba_solve(N, L.S, L.rd, L.y, L.ctl + 1, tr);
-    fail = L.ctl[1];
+    fail = ba_solve_gj(N, L, tr);
   }
-  ba_update(A, w, L.y, fail, dX_out);
+  ba_pose_update(A, w, L.M + n, ld, fail, dX_out);
 }
 
-// One F-BA iteration.  blockIdx < NL: Schur block; then patch owners; the
-// last workgroup to finish (when do_solve) runs the solve tail.
+// Schur blocks + (do_solve) the last-arrival solve tail.  One workgroup per
+// lower 6x6 block (a, b) of S.
 __global__ void __launch_bounds__(kIterThreads)
-    ba_iter_kernel(BaArgs A, BaWs w, double* S_out, double* y_out, double* dX_out, int do_solve,
-                   int trace_it) {
+    ba_schur_kernel(BaArgs A, BaWs w, double* S_out, double* y_out, double* dX_out, int do_solve,
+                    int it, int trace_it) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const IterLds L = iter_carve(lds, A.N);
-  const int N = A.N, NL = N * (N + 1) / 2, tid = threadIdx.x;
-  const Intr K{A.intrinsics[0], A.intrinsics[1], A.intrinsics[2], A.intrinsics[3]};
-  const int kmax = w.meta[3] - 1;
-  const double lam = (double)A.lmbda[0];
-  const int nuniq = w.meta[0];
+  const TailLds L = tail_carve(lds, A.N);
+  const int tid = threadIdx.x;
   int64_t* tr = trace_it ? w.tmark : nullptr;
   if (tid == 0) w.wgt[2 * blockIdx.x] = (int64_t)wall_clock64();
-  if ((int)blockIdx.x < NL) {
+  {
     const int d = blockIdx.x, a = tri_row(d), b = d - a * (a + 1) / 2;
+    const double lam = (double)A.lmbda[0];
+    const int nuniq = w.meta[0];
     double acc[42];  // 36 S entries + 6 y entries
 #pragma unroll
     for (int i = 0; i < 42; i++) acc[i] = 0.0;
-    for (int u = tid; u < nuniq; u += blockDim.x) {
-      const unsigned mask = w.pmask[u];
-      if (((mask >> a) & 1u) && ((mask >> b) & 1u))
-        patch_schur_terms(A, w, K, kmax, lam, u, a, b, acc, acc + 36);
+    // compact the patches whose mask holds a and b (ballots, in patch order)
+    int* rp = reinterpret_cast<int*>(L.M);  // free until the tail
+    int* wc = L.ctl + 8;                    // per-wave counts
+    const int lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+    int nrel = 0;
+    for (int base = 0; base < nuniq; base += blockDim.x) {
+      const int u = base + tid;
+      bool rel = false;
+      if (u < nuniq) {
+        const unsigned mask = w.pmask[u];
+        rel = ((mask >> a) & 1u) && ((mask >> b) & 1u);
+      }
+      const unsigned long long m = __ballot(rel);
+      if (lane == 0) wc[wid] = __popcll(m);
+      __syncthreads();
+      int before = 0, total = 0;
+      for (int k = 0; k < nw; k++) {
+        const int c = wc[k];
+        before += (k < wid) ? c : 0;
+        total += c;
+      }
+      if (rel) rp[nrel + before + __popcll(m & ((1ull << lane) - 1ull))] = u;
+      nrel += total;
+      __syncthreads();
     }
-    block_sum<42>(acc, L.part, L.S);
-    if (tid < 36) S_out[36 * d + tid] = L.S[tid];
-    if (a == b && tid >= 36 && tid < 42) y_out[6 * a + tid - 36] = L.S[tid];
-  } else {
-    const int u = (blockIdx.x - NL) * blockDim.x + tid;
-    if (u < nuniq) patch_owner_terms(A, w, K, kmax, lam, u);
+    int64_t* trw = (blockIdx.x == 0) ? tr : (blockIdx.x == gridDim.x - 1 && tr ? tr + 5 : nullptr);
+    trace(trw, 100);
+    const double* EC = w.EC[it & 1];
+    for (int i = tid; i < nrel; i += blockDim.x)
+      patch_schur_terms(w, EC, A.t0, lam, rp[i], a, b, acc);
+    __syncthreads();  // rp is overwritten by the sums below
+    trace(trw, 101);
+    double* red = L.M;  // 42 doubles, free until the tail
+    // every thread with data has tid < nrel (one patch per thread when
+    // nrel <= blockDim, more otherwise: then all waves are active)
+    const int active = nrel >= (int)blockDim.x ? (int)(blockDim.x >> 6) : (nrel + 63) / 64;
+    block_sum<42>(acc, L.part, red, active);
+    if (tid < 36) S_out[36 * d + tid] = red[tid];
+    if (a == b && tid >= 36 && tid < 42) y_out[6 * a + tid - 36] = red[tid];
+    trace(trw, 102);
   }
   __syncthreads();
   if (tid == 0) w.wgt[2 * blockIdx.x + 1] = (int64_t)wall_clock64();
@@ -983,17 +995,18 @@ __global__ void __launch_bounds__(kIterThreads)
   if (tid == 0) L.ctl[0] = (atomicAdd(&w.meta[4], 1) == (int)gridDim.x - 1) ? 1 : 0;
   __syncthreads();
   if (!L.ctl[0]) return;
-  __threadfence();  // acquire: every other workgroup's S blocks, Q, U, c
+  __threadfence();  // acquire: every other workgroup's S blocks and y
   trace(tr, 49);
   ba_solve_tail(A, w, S_out, y_out, dX_out, L, tr);
+  trace(tr, 52);
   if (tid == 0) w.meta[4] = 0;  // ticket for the next launch
 }
 
-// split form, step 3: solve + update from an (all-reduced) S, y
+// split form, step 3 (and N == 0): solve + update from an (all-reduced) S, y
 __global__ void __launch_bounds__(kIterThreads)
     ba_solve_kernel(BaArgs A, BaWs w, const double* S_in, const double* y_in, double* dX_out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const IterLds L = iter_carve(lds, A.N);
+  const TailLds L = tail_carve(lds, A.N);
   ba_solve_tail(A, w, S_in, y_in, dX_out, L, nullptr);
 }
 
@@ -1048,7 +1061,7 @@ static void ensure_lds_limits() {
   if (done) return;
   (void)hipFuncSetAttribute((const void*)ba_setup_kernel,
                             hipFuncAttributeMaxDynamicSharedMemorySize, kSetupLds);
-  (void)hipFuncSetAttribute((const void*)ba_iter_kernel,
+  (void)hipFuncSetAttribute((const void*)ba_schur_kernel,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)ba_solve_kernel,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1084,7 +1097,8 @@ static BaArgs make_args(float* poses, float* patches, const float* intrinsics, c
   return a;
 }
 
-static int iter_grid(int E, int N) { return N * (N + 1) / 2 + (E + kIterThreads - 1) / kIterThreads; }
+static int schur_grid(int N) { return N * (N + 1) / 2; }
+static int lin_grid(int E) { return (E + 255) / 256; }
 
 DPVO_EXPORT size_t dpvo_ba_workspace_bytes(int E, int t0, int t1) {
   const int N = t1 > t0 ? t1 - t0 : 0;
@@ -1126,8 +1140,12 @@ DPVO_EXPORT int dpvo_ba_build_schur(const float* poses, const float* patches,
   ensure_lds_limits();
   BaArgs a = make_args(const_cast<float*>(poses), const_cast<float*>(patches), intrinsics, target,
                        weight, lmbda, ii, jj, kk, E, P, num_poses, 0, t0, t1);
-  hipLaunchKernelGGL(ba_iter_kernel, dim3(iter_grid(E, N)), dim3(kIterThreads), iter_lds(N),
-                     as_stream(stream), a, w, S_lower ? S_lower : w.S, y ? y : w.y, nullptr, 0, 0);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(ba_lin_kernel, dim3(lin_grid(E)), dim3(256), 0, s, a, w, 0);
+  int st = launch_status();
+  if (st || N == 0) return st;
+  hipLaunchKernelGGL(ba_schur_kernel, dim3(schur_grid(N)), dim3(kIterThreads), iter_lds(N), s, a,
+                     w, S_lower ? S_lower : w.S, y ? y : w.y, nullptr, 0, 0, 0);
   return launch_status();
 }
 
@@ -1141,10 +1159,16 @@ DPVO_EXPORT int dpvo_ba_solve_update(float* poses, float* patches, const double*
   BaWs w;
   ba_layout(E, N, (char*)workspace, &w);
   ensure_lds_limits();
+  // the patch retraction reads lmbda (Q = 1/(C + lmbda)) from the workspace
+  // copy the build step made
   BaArgs a = make_args(poses, patches, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                        nullptr, E, P, num_poses, 0, t0, t1);
-  hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(kIterThreads), iter_lds(N), as_stream(stream),
-                     a, w, S_lower ? S_lower : w.S, y ? y : w.y, dX_out);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(kIterThreads), iter_lds(N), s, a, w,
+                     S_lower ? S_lower : w.S, y ? y : w.y, dX_out);
+  int st = launch_status();
+  if (st) return st;
+  hipLaunchKernelGGL(ba_apply_kernel, dim3(lin_grid(E)), dim3(256), 0, s, a, w, 1);
   return launch_status();
 }
 
@@ -1177,7 +1201,7 @@ DPVO_EXPORT int dpvo_ba_workgroup_marks(const void* workspace, int E, int t0, in
   const int N = t1 > t0 ? t1 - t0 : 0;
   BaWs w;
   ba_layout(E, N, (char*)workspace, &w);
-  return hipMemcpyAsync(out, w.wgt, sizeof(int64_t) * 2 * iter_grid(E, N),
+  return hipMemcpyAsync(out, w.wgt, sizeof(int64_t) * 2 * schur_grid(N),
                         hipMemcpyDeviceToDevice, as_stream(stream)) == hipSuccess
              ? DPVO_OK
              : DPVO_ERR_LAUNCH;
@@ -1208,8 +1232,14 @@ DPVO_EXPORT int dpvo_ba_forward(float* poses, float* patches, const float* intri
                      pow2_at_least(E < 2 ? 2 : E));
   int st = launch_status();
   for (int it = 0; it < iterations && st == DPVO_OK; it++) {
-    hipLaunchKernelGGL(ba_iter_kernel, dim3(iter_grid(E, N)), dim3(kIterThreads), iter_lds(N), s,
-                       a, w, w.S, w.y, nullptr, 1, it == 0 ? 1 : 0);
+    hipLaunchKernelGGL(ba_lin_kernel, dim3(lin_grid(E)), dim3(256), 0, s, a, w, it);
+    if (N > 0)  // N == 0 (structure only): dZ = Q u, applied by the next lin / apply kernel
+      hipLaunchKernelGGL(ba_schur_kernel, dim3(schur_grid(N)), dim3(kIterThreads), iter_lds(N), s,
+                         a, w, w.S, w.y, nullptr, 1, it, it == 0 ? 1 : 0);
+    st = launch_status();
+  }
+  if (st == DPVO_OK) {
+    hipLaunchKernelGGL(ba_apply_kernel, dim3(lin_grid(E)), dim3(256), 0, s, a, w, iterations);
     st = launch_status();
   }
   return st;

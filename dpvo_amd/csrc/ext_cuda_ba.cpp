@@ -68,7 +68,7 @@ std::vector<torch::Tensor> ba_forward(torch::Tensor poses, torch::Tensor patches
   return {};
 }
 
-// Same call; returns the 64 phase marks followed by the per-workgroup marks (100 MHz ticks:
+// Same call; returns the 128 phase marks followed by the per-workgroup marks (100 MHz ticks:
 // start, setup, then linearize/patch/schur/solve/update per iteration).
 torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
                                torch::Tensor intrinsics, torch::Tensor target, torch::Tensor weight,
@@ -77,13 +77,13 @@ torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
                                bool eff_impl) {
   auto ws = ba_forward_ws(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, PPF, t0,
                           t1, iterations, eff_impl);
-  auto out = torch::zeros({64}, poses.options().dtype(torch::kInt64));
+  auto out = torch::zeros({128}, poses.options().dtype(torch::kInt64));
   if (!ws.defined()) return out;
   check_status(dpvo_ba_phase_marks(ws.data_ptr(), ii.numel(), t0, t1, out.data_ptr<int64_t>(),
                                    current_stream()),
                "cuda_ba.forward_marks");
   const int N = t1 - t0, E = ii.numel();
-  const int64_t grid = N * (N + 1) / 2 + (E + 511) / 512;
+  const int64_t grid = N * (N + 1) / 2;
   auto wg = torch::zeros({2 * grid}, out.options());
   check_status(dpvo_ba_workgroup_marks(ws.data_ptr(), E, t0, t1, wg.data_ptr<int64_t>(),
                                        current_stream()),

@@ -135,14 +135,14 @@ int dpvo_ba_solve_update(float* poses, float* patches, const double* S_lower, co
    `out`: bit 0 = Cholesky failed in the last solve (dX was set to 0),
    bit 1 = some kk outside [0, num_patches) (clamped). */
 int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1, int* out, void* stream);
-/* Instrumentation (no reference counterpart): the 256 marks the last
+/* Instrumentation (no reference counterpart): the 128 marks the last
    dpvo_ba_forward on this workspace stamped -- wall clock (100 MHz): [0]
    start, [1] setup, then linearize, patch, schur, solve, update per iteration;
    shader clock: [38] start, [39] end; [40..] finer stamps inside the setup
    and the first solve -- copied to the DEVICE array `out`. */
 int dpvo_ba_phase_marks(const void* workspace, int E, int t0, int t1, int64_t* out, void* stream);
 /* Instrumentation: start / end wall-clock stamps of every workgroup of the
-   last iteration launch, [2 x (N(N+1)/2 + ceil(E/512))] int64 to DEVICE `out`. */
+   last Schur launch, [2 x N(N+1)/2] int64 to DEVICE `out`. */
 int dpvo_ba_workgroup_marks(const void* workspace, int E, int t0, int t1, int64_t* out,
                             void* stream);
 

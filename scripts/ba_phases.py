@@ -36,20 +36,25 @@ for rep in range(30):
         continue
     d = {"call (events)": e0.elapsed_time(e1) * 1e3}
     for name, a, b in [("setup.sort", 40, 41), ("setup.masks", 41, 42),
-                       ("setup -> solve tail", 42, 49), ("solve.factor0", 49, 50),
-                       ("solve.factorise", 50, 51), ("solve.substitute", 51, 52)]:
+                       ("setup end -> solve tail", 42, 49), ("tail: load + inv0", 49, 50),
+                       ("tail: gauss-jordan", 50, 51), ("tail: update", 51, 52)]:
         d[name] = (m[b] - m[a]) * 10.0 / 1000.0
-    wg = m[64:]
+    N = G.F - 1
+    for k in range(N):
+        d[f"gj.k{k:02d}.pivot"] = (m[60 + 2 * k] - (m[50] if k == 0 else m[59 + 2 * k])) * 0.01
+        d[f"gj.k{k:02d}.elim"] = (m[61 + 2 * k] - m[60 + 2 * k]) * 0.01
+    for nm, base in [("WG0", 100), ("WGlast", 105)]:
+        d[f"{nm}.compact"] = (m[base] - m[128 + 2 * (0 if nm == 'WG0' else (N * (N + 1) // 2 - 1))]) * 0.01
+        d[f"{nm}.gather"] = (m[base + 1] - m[base]) * 0.01
+        d[f"{nm}.sum"] = (m[base + 2] - m[base + 1]) * 0.01
+    wg = m[128:]
     NL = (G.F - 1) * G.F // 2
     starts, ends = wg[0::2], wg[1::2]
     t0 = min(starts)
     dur = [(e - s) * 0.01 for s, e in zip(starts, ends)]
     d["iter: first WG start -> last WG end"] = (max(ends) - t0) * 0.01
-    d["iter: diag WG max dur"] = max(dur[i] for i in range(NL)
-                                     if i == (int((8 * i + 1) ** 0.5 - 1) // 2) *
-                                     ((int((8 * i + 1) ** 0.5 - 1) // 2) + 3) // 2)
-    d["iter: off WG max dur"] = max(dur[:NL])
-    d["iter: owner WG max dur"] = max(dur[NL:])
+    d["iter: Schur WG max dur"] = max(dur)
+    d["iter: Schur WG min dur"] = min(dur)
     d["iter: WG start spread"] = (max(starts) - t0) * 0.01
     for k, v in d.items():
         acc.setdefault(k, []).append(v)
