@@ -989,13 +989,18 @@ __global__ void __launch_bounds__(kIterThreads)
   __syncthreads();
   if (tid == 0) w.wgt[2 * blockIdx.x + 1] = (int64_t)wall_clock64();
   if (!do_solve) return;
-  // last-arrival election: release this workgroup's writes, take a ticket
-  __threadfence();
+  // last-arrival election.  Every wave drains its stores (workgroup-scope
+  // release: s_waitcnt), then ONE lane writes the XCD L2 back (agent-scope
+  // release, ~1.7 us -- per workgroup, not per thread) and takes a ticket.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
-  if (tid == 0) L.ctl[0] = (atomicAdd(&w.meta[4], 1) == (int)gridDim.x - 1) ? 1 : 0;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    L.ctl[0] = (atomicAdd(&w.meta[4], 1) == (int)gridDim.x - 1) ? 1 : 0;
+    if (L.ctl[0]) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this CU's L1
+  }
   __syncthreads();
-  if (!L.ctl[0]) return;
-  __threadfence();  // acquire: every other workgroup's S blocks and y
+  if (!L.ctl[0]) return;  // the last one reads every other workgroup's S blocks and y
   trace(tr, 49);
   ba_solve_tail(A, w, S_out, y_out, dX_out, L, tr);
   trace(tr, 52);
