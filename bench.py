@@ -91,13 +91,18 @@ def main():
     D = G.to(dev)
     P = G.patches.shape[-1]
     C = 128
-    pyr = synthetic.make_features(mem=args.mem, C=C, levels=levels, seed=args.seed, device=dev)
+    # the network emits NCHW features; the ring buffer keeps them channels-last
+    # (corr_nhwc.hip).  Every step re-inserts one frame (NCHW -> channels-last)
+    # so the per-frame cost of that layout is inside the timed region.
+    pyr_nchw = synthetic.make_features(mem=args.mem, C=C, levels=levels, seed=args.seed,
+                                       device=dev)
+    pyr = [synthetic.channels_last(p) for p in pyr_nchw]
     # gmap: patch features of every (frame, slot), DPVO's pmem = mem ring
     gbuf = torch.zeros(1, args.mem * G.M, C, P, P, device=dev)
     centres = D.patches[: G.F * G.M, :2, P // 2, P // 2]  # [F*M, 2] (x, y)
     for f in range(G.F):
         gbuf[0, f * G.M:(f + 1) * G.M] = altcorr.patchify(
-            pyr[0][:, f], centres[f * G.M:(f + 1) * G.M].unsqueeze(0), P // 2)[0]
+            pyr_nchw[0][:, f], centres[f * G.M:(f + 1) * G.M].unsqueeze(0), P // 2)[0]
     lmbda = torch.tensor([1e-4], device=dev)
     poses, patches = D.poses.clone(), D.patches.clone()
     kk1 = D.kk % (G.M * args.mem)  # dpvo.py:456-457
@@ -108,6 +113,9 @@ def main():
                for _ in range(args.steps)]
 
     def step(i=None):
+        slot = (i or 0) % args.mem  # frame insertion (dpvo.py:__call__ -> ring buffer)
+        for src, dst in zip(pyr_nchw, pyr):
+            altcorr.to_channels_last(src[0, slot], dst[0, slot])
         coords = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk)
         if i is not None:
             ev_corr[i][0].record()
@@ -180,7 +188,7 @@ def main():
                 "parallelism": f"replicas x{world}",
             },
             "roofline": {
-                "kernel": "corr_fwd_levels_kernel (A-CORR, all levels, one launch)",
+                "kernel": "corr_nhwc_kernel (A-CORR, all levels, one launch)",
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,

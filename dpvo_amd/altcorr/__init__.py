@@ -3,7 +3,8 @@
 Same entry points as dpvo/altcorr/correlation.py of cuteboyqq/DPVO
 (`corr`, `patchify`, `CorrLayer`, `PatchLayer`), backed by the `cuda_corr`
 HIP extension.  Extra: `corr_levels`, the fused all-levels call of
-DPVO.corr (dpvo/dpvo.py:456-465) in one launch.
+DPVO.corr (dpvo/dpvo.py:456-465) in one launch, and `to_channels_last`
+(pyramids stored channels-last take the matrix-core correlation path).
 """
 from .correlation import (  # noqa: F401
     BORDER_MODE,
@@ -12,4 +13,5 @@ from .correlation import (  # noqa: F401
     corr,
     corr_levels,
     patchify,
+    to_channels_last,
 )

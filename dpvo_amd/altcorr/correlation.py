@@ -89,10 +89,26 @@ def corr(fmap1, fmap2, coords, ii, jj, radius=1, dropout=1):
     return CorrLayer.apply(fmap1, fmap2, coords, ii, jj, radius, dropout)
 
 
+def to_channels_last(src, dst=None):
+    """Copy a [..., C, H, W] feature map into channels-last memory (HIP
+    transpose); ``dst`` (same shape, channels-last) is filled in place, e.g.
+    one frame slot of a channels-last pyramid ring buffer."""
+    require_gpu(src)
+    if dst is None:
+        perm = list(range(src.dim() - 3)) + [src.dim() - 2, src.dim() - 1, src.dim() - 3]
+        inv = [perm.index(i) for i in range(src.dim())]
+        dst = src.new_empty([src.shape[i] for i in perm]).permute(inv)
+    cuda_corr.feature_to_nhwc(src, dst)
+    return dst
+
+
 def corr_levels(fmap1, pyramid, coords, ii, jj, radius=3, scales=(1, 4)):
     """DPVO.corr (dpvo/dpvo.py:456-465) in ONE launch: correlation of every
     pyramid level (coords divided by each level's scale) stacked on the last
-    axis and flattened to [B, M, (2R+1)^2 * p^2 * L] float32.  Inference only."""
+    axis and flattened to [B, M, (2R+1)^2 * p^2 * L] float32.  Inference only.
+
+    Levels stored channels-last (``synthetic.channels_last`` / ``to_channels_last``)
+    take the matrix-core path (corr_nhwc.hip); NCHW levels the VALU path."""
     require_gpu(fmap1)
     out = cuda_corr.forward_levels(fmap1, list(pyramid), coords, ii, jj, radius,
                                    [float(s) for s in scales])

@@ -38,6 +38,29 @@ std::vector<torch::Tensor> corr_forward(torch::Tensor fmap1, torch::Tensor fmap2
 
 // Fused multi-level form (dpvo/dpvo.py:462-465): returns [B, M, Dp, Dp, H, W, L]
 // float32 = torch.stack([corr(level l) for l], -1).
+// src [..., C, H, W] contiguous -> dst: same shape, channels-last memory
+// (dst.permute(..., H, W, C) contiguous), e.g. one frame of a pyramid level.
+void feature_to_nhwc(torch::Tensor src, torch::Tensor dst) {
+  check_device(src, "src");
+  check_device(dst, "dst");
+  TORCH_CHECK(src.dim() >= 3 && src.sizes() == dst.sizes(), "src / dst shapes differ");
+  TORCH_CHECK(src.scalar_type() == dst.scalar_type(), "src / dst dtypes differ");
+  const int d = src.dim();
+  std::vector<int64_t> perm;
+  for (int i = 0; i < d - 3; i++) perm.push_back(i);
+  perm.push_back(d - 2);
+  perm.push_back(d - 1);
+  perm.push_back(d - 3);
+  TORCH_CHECK(dst.permute(perm).is_contiguous(), "dst must be channels-last");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(src.device());
+  src = src.contiguous();
+  const int C = src.size(d - 3), H = src.size(d - 2), W = src.size(d - 1);
+  const int count = src.numel() / ((int64_t)C * H * W);
+  check_status(dpvo_feature_to_nhwc(src.data_ptr(), dst.data_ptr(), count, C, H, W,
+                                    dtype_code(src), current_stream()),
+               "cuda_corr.feature_to_nhwc");
+}
+
 torch::Tensor corr_forward_levels(torch::Tensor fmap1, std::vector<torch::Tensor> fmap2,
                                   torch::Tensor coords, torch::Tensor ii, torch::Tensor jj,
                                   int radius, std::vector<double> scales) {
@@ -54,18 +77,36 @@ torch::Tensor corr_forward_levels(torch::Tensor fmap1, std::vector<torch::Tensor
   std::vector<const void*> ptrs(L);
   std::vector<int> H2(L), W2(L);
   std::vector<float> sc(L);
+  const int B = coords.size(0), M = coords.size(1), H = coords.size(3), W = coords.size(4);
+  const int Dp = 2 * radius + 1;
+  auto out = torch::empty({B, M, Dp, Dp, H, W, L}, fmap1.options().dtype(torch::kFloat32));
+  // channels-last pyramid ([B,N,C,H,W] view of [B,N,H,W,C] memory): matrix-core path
+  bool nhwc = true;
   for (int l = 0; l < L; l++) {
     check_device(fmap2[l], "fmap2");
+    TORCH_CHECK(fmap2[l].dim() == 5, "fmap2 levels must be [B,N,C,H,W]");
     TORCH_CHECK(fmap2[l].scalar_type() == fmap1.scalar_type(), "fmap dtype mismatch");
-    fmap2[l] = fmap2[l].contiguous();
-    ptrs[l] = fmap2[l].data_ptr();
+    nhwc = nhwc && fmap2[l].permute({0, 1, 3, 4, 2}).is_contiguous() && fmap2[l].size(2) > 1;
     H2[l] = fmap2[l].size(3);
     W2[l] = fmap2[l].size(4);
     sc[l] = (float)scales[l];
   }
-  const int B = coords.size(0), M = coords.size(1), H = coords.size(3), W = coords.size(4);
-  const int Dp = 2 * radius + 1;
-  auto out = torch::empty({B, M, Dp, Dp, H, W, L}, fmap1.options().dtype(torch::kFloat32));
+  if (nhwc) {
+    for (int l = 0; l < L; l++) ptrs[l] = fmap2[l].data_ptr();
+    const int st = dpvo_corr_forward_levels_nhwc(
+        fmap1.data_ptr(), ptrs.data(), H2.data(), W2.data(), sc.data(), L,
+        coords.data_ptr<float>(), ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), B, M,
+        fmap1.size(2), H, W, fmap1.size(1), fmap2[0].size(1), radius, dtype_code(fmap1),
+        out.data_ptr<float>(), current_stream());
+    if (st != DPVO_ERR_UNSUPPORTED) {
+      check_status(st, "cuda_corr.forward_levels");
+      return out;
+    }
+  }
+  for (int l = 0; l < L; l++) {
+    fmap2[l] = fmap2[l].contiguous();
+    ptrs[l] = fmap2[l].data_ptr();
+  }
   check_status(dpvo_corr_forward_levels(fmap1.data_ptr(), ptrs.data(), H2.data(), W2.data(),
                                         sc.data(), L, coords.data_ptr<float>(),
                                         ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), B, M,
@@ -166,6 +207,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("patchify_backward", &patchify_backward, "PATCHIFY backward");
   // additions (not in the reference surface)
   m.def("forward_levels", &corr_forward_levels, "CORR forward, all pyramid levels in one launch");
+  m.def("feature_to_nhwc", &feature_to_nhwc, "[..., C, H, W] -> channels-last copy into dst");
   m.def("patchify_forward_clamped", &patchify_forward_clamped, "PATCHIFY forward, border clamp");
   m.def("patchify_backward_clamped", &patchify_backward_clamped, "PATCHIFY backward, border clamp");
   m.attr("native_library") = dpvo_version();

@@ -161,3 +161,10 @@ def make_features(mem=36, C=128, H=120, W=160, levels=(1, 4), seed=0, device="cu
         else:
             pyr.append(torch.nn.functional.avg_pool2d(f1[0], s, s).unsqueeze(0))
     return [p.to(dtype).contiguous() for p in pyr]
+
+
+def channels_last(level):
+    """[B, N, C, H, W] -> the same tensor in channels-last memory
+    ([B, N, H, W, C] storage; what cuda_corr.forward_levels' matrix-core path
+    reads)."""
+    return level.permute(0, 1, 3, 4, 2).contiguous().permute(0, 1, 4, 2, 3)

@@ -68,6 +68,22 @@ int dpvo_corr_forward_levels(const void* fmap1, const void* const* fmap2, const 
                              int W, int N1, int N2, int radius, int dtype, float* out,
                              void* stream);
 
+/* A-CORR, all levels, channels-last pyramid (no reference counterpart: the
+   layout is this build's; semantics identical to dpvo_corr_forward_levels).
+   fmap2[l] is [B,N2,H2[l],W2[l],C] (a [B,N2,C,H,W] tensor in channels-last
+   memory), fp32, C == 128, L <= 4, H*W <= 16, (2R+1)^2*H*W <= 512.
+   Returns DPVO_ERR_UNSUPPORTED outside that envelope (callers fall back to
+   dpvo_corr_forward_levels on NCHW data). */
+int dpvo_corr_forward_levels_nhwc(const void* fmap1, const void* const* fmap2, const int* H2,
+                                  const int* W2, const float* scale, int L, const float* coords,
+                                  const int64_t* ii, const int64_t* jj, int B, int M, int C,
+                                  int H, int W, int N1, int N2, int radius, int dtype, float* out,
+                                  void* stream);
+/* Feature maps [count,C,H,W] -> channels-last [count,H,W,C] (the per-frame
+   cost of keeping a channels-last pyramid; dtype F32 or F16). */
+int dpvo_feature_to_nhwc(const void* src, void* dst, int count, int C, int H, int W, int dtype,
+                         void* stream);
+
 /* A-CORR-BWD.  Replaces cuda_corr.backward (correlation.cpp:58,
    correlation_kernel.cu:275-325 + corr_backward_kernel :178-229).
    grad [B,M,2R+1,2R+1,H,W] float32.  fmap1_grad / fmap2_grad are ZEROED by

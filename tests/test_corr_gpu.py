@@ -189,3 +189,48 @@ def test_autograd_wrappers(gpu):
     c2 = torch.rand(1, 10, 2, device=gpu) * 18 + 1
     p = altcorr.patchify(net, c2, 1)
     assert p.shape == (1, 10, 8, 3, 3)
+
+
+# ---- channels-last pyramid: matrix-core path (corr_nhwc.hip) ----
+@pytest.mark.parametrize("kw", [dict(), dict(spread=4.0), dict(far=0.3),
+                                dict(M=130, H2=12, W2=14)])
+@pytest.mark.parametrize("levels", [(1,), (1, 4), (1, 2, 4, 8)])
+def test_channels_last_levels_match_oracle(gpu, kw, levels):
+    from dpvo_amd import altcorr, synthetic
+
+    f1, f2, co, ii, jj, R = _case(11, **{**dict(M=67, C=128, H2=40, W2=48), **kw})
+    lv1 = _t(f2, gpu)
+    pyr = [lv1 if s == 1 else torch.nn.functional.avg_pool2d(lv1[0], s, s).unsqueeze(0)
+           for s in levels]
+    pyr_cl = [synthetic.channels_last(p) for p in pyr]
+    out = altcorr.corr_levels(_t(f1, gpu), pyr_cl, _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R,
+                              scales=levels)
+    out = out.view(1, len(ii), 2 * R + 1, 2 * R + 1, 3, 3, len(levels)).cpu().numpy()
+    for l, s in enumerate(levels):
+        ref = oracle.corr_fwd(f1, pyr[l].cpu().numpy(), co / s, ii, jj, R)
+        _close(out[..., l], ref, 1e-5)
+
+
+def test_channels_last_equals_nchw_path(cc, gpu):
+    from dpvo_amd import altcorr, synthetic
+
+    f1, f2, co, ii, jj, R = _case(12, M=200, C=128, H2=60, W2=80)
+    lv1 = _t(f2, gpu)
+    pyr = [lv1, torch.nn.functional.avg_pool2d(lv1[0], 4, 4).unsqueeze(0).contiguous()]
+    a = altcorr.corr_levels(_t(f1, gpu), pyr, _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R, (1, 4))
+    b = altcorr.corr_levels(_t(f1, gpu), [synthetic.channels_last(p) for p in pyr], _t(co, gpu),
+                            _t(ii, gpu), _t(jj, gpu), R, (1, 4))
+    err = (a - b).abs().max().item()
+    assert err <= 1e-5 * max(1.0, a.abs().max().item()), err
+
+
+def test_to_channels_last_frame_slot(gpu):
+    from dpvo_amd import altcorr, synthetic
+
+    src = torch.randn(1, 5, 128, 30, 40, device=gpu)
+    dst = synthetic.channels_last(torch.zeros_like(src))
+    altcorr.to_channels_last(src[0, 3], dst[0, 3])  # one frame of a ring buffer
+    assert torch.equal(dst[0, 3], src[0, 3])
+    assert torch.count_nonzero(dst[0, :3]) == 0
+    full = altcorr.to_channels_last(src)
+    assert torch.equal(full, src) and full.permute(0, 1, 3, 4, 2).is_contiguous()
