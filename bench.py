@@ -92,8 +92,9 @@ def main():
     P = G.patches.shape[-1]
     C = 128
     # the network emits NCHW features; the ring buffer keeps them channels-last
-    # (corr_nhwc.hip).  Every step re-inserts one frame (NCHW -> channels-last)
-    # so the per-frame cost of that layout is inside the timed region.
+    # (corr_nhwc.hip).  Every step inserts one frame (NCHW level 1 -> pooled,
+    # channels-last levels, one launch) so the per-frame cost of the pyramid and
+    # its layout is inside the timed region.
     pyr_nchw = synthetic.make_features(mem=args.mem, C=C, levels=levels, seed=args.seed,
                                        device=dev)
     pyr = [synthetic.channels_last(p) for p in pyr_nchw]
@@ -114,8 +115,7 @@ def main():
 
     def step(i=None):
         slot = (i or 0) % args.mem  # frame insertion (dpvo.py:__call__ -> ring buffer)
-        for src, dst in zip(pyr_nchw, pyr):
-            altcorr.to_channels_last(src[0, slot], dst[0, slot])
+        altcorr.insert_frame(pyr_nchw[0][0, slot], pyr, slot, levels)
         coords = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk)
         if i is not None:
             ev_corr[i][0].record()

@@ -4,7 +4,8 @@ Same entry points as dpvo/altcorr/correlation.py of cuteboyqq/DPVO
 (`corr`, `patchify`, `CorrLayer`, `PatchLayer`), backed by the `cuda_corr`
 HIP extension.  Extra: `corr_levels`, the fused all-levels call of
 DPVO.corr (dpvo/dpvo.py:456-465) in one launch, and `to_channels_last`
-(pyramids stored channels-last take the matrix-core correlation path).
+(pyramids stored channels-last take the matrix-core correlation path), and
+`insert_frame`, the one-launch channels-last frame insertion of all levels.
 """
 from .correlation import (  # noqa: F401
     BORDER_MODE,
@@ -12,6 +13,7 @@ from .correlation import (  # noqa: F401
     PatchLayer,
     corr,
     corr_levels,
+    insert_frame,
     patchify,
     to_channels_last,
 )

@@ -102,6 +102,17 @@ def to_channels_last(src, dst=None):
     return dst
 
 
+def insert_frame(fmap, pyramid, slot, scales=(1, 4)):
+    """Write one new frame into a channels-last pyramid ring buffer in ONE
+    launch: level s of ring slot ``slot`` = avg_pool2d(fmap, s, s) (level 1 =
+    fmap itself), the frame insertion of dpvo.py (fmap1_/fmap2_ ring writes,
+    dpvo.py:462-463 read them back).  ``fmap`` is the NCHW [C, H, W] level-1
+    frame; ``pyramid[l]`` are [B, mem, C, H/s, W/s] channels-last buffers."""
+    require_gpu(fmap)
+    cuda_corr.feature_pyramid_insert(fmap, [p[0, slot] for p in pyramid],
+                                     [int(s) for s in scales])
+
+
 def corr_levels(fmap1, pyramid, coords, ii, jj, radius=3, scales=(1, 4)):
     """DPVO.corr (dpvo/dpvo.py:456-465) in ONE launch: correlation of every
     pyramid level (coords divided by each level's scale) stacked on the last

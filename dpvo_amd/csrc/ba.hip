@@ -1056,7 +1056,26 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// ba_fused.hip: the single-workgroup whole-call kernel for DPVO-sized windows
+size_t ba_fused_scratch_bytes(int E, int N);
+bool ba_fused_supported(int E, int N, int P);
+int ba_fused_launch(float* poses, float* patches, const float* intrinsics, const float* target,
+                    const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
+                    const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
+                    int iterations, char* scratch, int* meta, int64_t* marks, void* stream);
+// ba_blocks.hip: one persistent workgroup per lower 6x6 block of S
+size_t ba_blocks_scratch_bytes(int E, int N);
+bool ba_blocks_supported(int E, int N, int P);
+int ba_blocks_launch(float* poses, float* patches, const float* intrinsics, const float* target,
+                     const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
+                     const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
+                     int iterations, char* scratch, int* meta, int64_t* marks, void* stream);
+
 }  // namespace dpvo
+
+namespace {
+int g_ba_path = 0;  // 0 auto (blocks), 1 fused single workgroup, 2 multi-kernel, 3 blocks
+}
 
 using namespace dpvo;
 
@@ -1107,7 +1126,15 @@ static int lin_grid(int E) { return (E + 255) / 256; }
 
 DPVO_EXPORT size_t dpvo_ba_workspace_bytes(int E, int t0, int t1) {
   const int N = t1 > t0 ? t1 - t0 : 0;
-  return ba_layout(E > 0 ? E : 1, N, nullptr, nullptr);
+  const int Ep = E > 0 ? E : 1;
+  const size_t a = ba_fused_scratch_bytes(Ep, N), b = ba_blocks_scratch_bytes(Ep, N);
+  return ba_layout(Ep, N, nullptr, nullptr) + (a > b ? a : b);
+}
+
+DPVO_EXPORT int dpvo_ba_select_path(int mode) {
+  if (mode < 0 || mode > 3) return DPVO_ERR_INVALID;
+  g_ba_path = mode;
+  return DPVO_OK;
 }
 
 DPVO_EXPORT int dpvo_ba_max_free_poses(void) { return kMaxFree; }
@@ -1228,7 +1255,15 @@ DPVO_EXPORT int dpvo_ba_forward(float* poses, float* patches, const float* intri
   if (E > kMaxSetupE || N > kMaxFree) return DPVO_ERR_UNSUPPORTED;
   if (workspace_bytes < dpvo_ba_workspace_bytes(E, t0, t1)) return DPVO_ERR_WORKSPACE;
   BaWs w;
-  ba_layout(E, N, (char*)workspace, &w);
+  const size_t base_bytes = ba_layout(E, N, (char*)workspace, &w);
+  if ((g_ba_path == 0 || g_ba_path == 3) && ba_blocks_supported(E, N, P))
+    return ba_blocks_launch(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
+                            num_poses, num_patches, t0, t1, iterations,
+                            (char*)workspace + base_bytes, w.meta, w.tmark, stream);
+  if (g_ba_path == 1 && ba_fused_supported(E, N, P))
+    return ba_fused_launch(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
+                           num_poses, num_patches, t0, t1, iterations,
+                           (char*)workspace + base_bytes, w.meta, w.tmark, stream);
   ensure_lds_limits();
   hipStream_t s = as_stream(stream);
   BaArgs a = make_args(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,

@@ -236,6 +236,66 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Frame insertion of a channels-last pyramid (dpvo.py frame insertion: the
+// level-1 fmap written into the ring slot, level s = avg_pool2d(fmap, s, s),
+// dpvo.py __call__ / net.py:411).  One launch for every level: a workgroup
+// stages an 8 x 32 pixel x 32 channel tile of the NCHW level-1 frame in LDS
+// (coalesced 128-B row reads), writes the channels-last level-1 pixels and
+// every pooled level whose s x s windows the tile holds (s | 8, s | 32), as
+// 128-B channel runs.  Pool order = torch's avg_pool2d (row-major sum in
+// fp32, then / s^2), so the pooled levels are bit-identical to it.
+// ---------------------------------------------------------------------------
+constexpr int kInsTY = 8, kInsTX = 32, kInsTC = 32;
+constexpr int kInsCS = kInsTY * kInsTX + 1;  // channel stride (+1: no bank conflicts)
+
+struct InsLevels {
+  float* dst[kMaxL];
+  int s[kMaxL];
+};
+
+__global__ void __launch_bounds__(256)
+    pyramid_insert_kernel(const float* __restrict__ src, InsLevels lv, int L, int C, int H,
+                          int W) {
+  __shared__ float tile[kInsTC * kInsCS];
+  const int tx0 = blockIdx.x * kInsTX, ty0 = blockIdx.y * kInsTY, c0 = blockIdx.z * kInsTC;
+  const int tid = threadIdx.x;
+  // load: 32 channels x 8 rows x 32 px (one 128-B row per 32 lanes)
+#pragma unroll 4
+  for (int k = tid; k < kInsTC * kInsTY * kInsTX; k += 256) {
+    const int x = k & 31, y = (k >> 5) & 7, c = k >> 8;
+    const int gx = tx0 + x, gy = ty0 + y, gc = c0 + c;
+    float v = 0.0f;
+    if (gx < W && gy < H && gc < C) v = src[((size_t)gc * H + gy) * W + gx];
+    tile[c * kInsCS + y * kInsTX + x] = v;
+  }
+  __syncthreads();
+  const int lane_c = tid & 31, grp = tid >> 5;  // 8 pixel groups of 32 channel lanes
+  const int gc = c0 + lane_c;
+  for (int l = 0; l < L; l++) {
+    const int s = lv.s[l];
+    const int Hs = H / s, Ws = W / s;
+    const int oy0 = ty0 / s, ox0 = tx0 / s, nty = kInsTY / s, ntx = kInsTX / s;
+    const float inv = (float)(s * s);
+    for (int q = grp; q < nty * ntx; q += 8) {
+      const int oy = oy0 + q / ntx, ox = ox0 + q % ntx;
+      if (oy >= Hs || ox >= Ws || gc >= C) continue;
+      const float* t = tile + lane_c * kInsCS + (q / ntx) * s * kInsTX + (q % ntx) * s;
+      float v;
+      if (s == 1) {
+        v = t[0];
+      } else {
+        float acc = 0.0f;
+        for (int a = 0; a < s; a++)
+          for (int b = 0; b < s; b++) acc += t[a * kInsTX + b];
+        v = acc / inv;
+      }
+      lv.dst[l][((size_t)oy * Ws + ox) * C + gc] = v;
+    }
+  }
+}
+
 }  // namespace dpvo
 
 using namespace dpvo;
@@ -287,4 +347,22 @@ DPVO_EXPORT int dpvo_feature_to_nhwc(const void* src, void* dst, int count, int 
       return launch_status();
   }
   return DPVO_ERR_UNSUPPORTED;
+}
+
+DPVO_EXPORT int dpvo_feature_pyramid_insert(const void* src, void* const* dst, const int* scale,
+                                            int L, int C, int H, int W, int dtype, void* stream) {
+  if (!src || !dst || !scale || L <= 0 || C <= 0 || H <= 0 || W <= 0) return DPVO_ERR_INVALID;
+  if (dtype != DPVO_F32 || L > kMaxL) return DPVO_ERR_UNSUPPORTED;
+  InsLevels lv = {};
+  for (int l = 0; l < L; l++) {
+    const int s = scale[l];
+    if (!dst[l]) return DPVO_ERR_INVALID;
+    if (s != 1 && s != 2 && s != 4 && s != 8) return DPVO_ERR_UNSUPPORTED;
+    lv.dst[l] = (float*)dst[l];
+    lv.s[l] = s;
+  }
+  const dim3 grid((W + kInsTX - 1) / kInsTX, (H + kInsTY - 1) / kInsTY, (C + kInsTC - 1) / kInsTC);
+  hipLaunchKernelGGL(pyramid_insert_kernel, grid, dim3(256), 0, as_stream(stream),
+                     (const float*)src, lv, L, C, H, W);
+  return launch_status();
 }

@@ -219,5 +219,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("last_status", &ba_last_status, "status word of the last BA on a workspace");
   m.def("max_free_poses", &dpvo_ba_max_free_poses);
   m.def("forward_marks", &ba_forward_marks, "forward + per-phase wall-clock marks");
+  m.def("select_path", [](int mode) { check_status(dpvo_ba_select_path(mode), "select_path"); },
+        "F-BA implementation: 0 auto (fused single-workgroup where supported), 2 multi-kernel");
   m.attr("native_library") = dpvo_version();
 }

@@ -61,6 +61,36 @@ void feature_to_nhwc(torch::Tensor src, torch::Tensor dst) {
                "cuda_corr.feature_to_nhwc");
 }
 
+// Frame insertion of a channels-last pyramid: src [C, H, W] (level-1 NCHW
+// frame), dst[l] [C, H/s, W/s] views in channels-last memory (one ring slot).
+void feature_pyramid_insert(torch::Tensor src, std::vector<torch::Tensor> dst,
+                            std::vector<int64_t> scales) {
+  check_device(src, "src");
+  TORCH_CHECK(src.dim() == 3, "src must be [C, H, W]");
+  TORCH_CHECK(dst.size() == scales.size() && !dst.empty(), "one scale per destination level");
+  TORCH_CHECK(src.scalar_type() == torch::kFloat32, "src must be float32");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(src.device());
+  src = src.contiguous();
+  const int C = src.size(0), H = src.size(1), W = src.size(2);
+  std::vector<void*> ptrs;
+  std::vector<int> sc;
+  for (size_t l = 0; l < dst.size(); l++) {
+    const torch::Tensor& d = dst[l];
+    check_device(d, "dst");
+    const int s = (int)scales[l];
+    TORCH_CHECK(d.scalar_type() == torch::kFloat32 && d.dim() == 3 && d.size(0) == C &&
+                    s > 0 && d.size(1) == H / s && d.size(2) == W / s,
+                "dst level ", l, " must be float32 [C, H/s, W/s]");
+    TORCH_CHECK(d.stride(0) == 1 && d.stride(2) == C && d.stride(1) == (int64_t)C * d.size(2),
+                "dst level ", l, " must be channels-last");
+    ptrs.push_back(d.data_ptr());
+    sc.push_back(s);
+  }
+  check_status(dpvo_feature_pyramid_insert(src.data_ptr(), ptrs.data(), sc.data(),
+                                           (int)ptrs.size(), C, H, W, DPVO_F32, current_stream()),
+               "cuda_corr.feature_pyramid_insert");
+}
+
 torch::Tensor corr_forward_levels(torch::Tensor fmap1, std::vector<torch::Tensor> fmap2,
                                   torch::Tensor coords, torch::Tensor ii, torch::Tensor jj,
                                   int radius, std::vector<double> scales) {
@@ -207,6 +237,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("patchify_backward", &patchify_backward, "PATCHIFY backward");
   // additions (not in the reference surface)
   m.def("forward_levels", &corr_forward_levels, "CORR forward, all pyramid levels in one launch");
+  m.def("feature_pyramid_insert", &feature_pyramid_insert,
+        "NCHW level-1 frame -> channels-last pyramid slot (all levels, one launch)");
   m.def("feature_to_nhwc", &feature_to_nhwc, "[..., C, H, W] -> channels-last copy into dst");
   m.def("patchify_forward_clamped", &patchify_forward_clamped, "PATCHIFY forward, border clamp");
   m.def("patchify_backward_clamped", &patchify_backward_clamped, "PATCHIFY backward, border clamp");

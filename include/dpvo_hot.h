@@ -84,6 +84,15 @@ int dpvo_corr_forward_levels_nhwc(const void* fmap1, const void* const* fmap2, c
 int dpvo_feature_to_nhwc(const void* src, void* dst, int count, int C, int H, int W, int dtype,
                          void* stream);
 
+/* Frame insertion of a channels-last pyramid (the ring-buffer writes of
+   dpvo.py __call__: fmap -> level 1, avg_pool2d(fmap, s, s) -> level s,
+   net.py:411 / dpvo.py:462-463) in one launch.  src: one NCHW level-1 frame
+   [C, H, W] fp32; dst[l]: the channels-last slot [H/s, W/s, C] of level l,
+   scale[l] in {1, 2, 4, 8}.  Pooling sums row-major in fp32 and divides by
+   s^2 (torch avg_pool2d order: bit-identical). */
+int dpvo_feature_pyramid_insert(const void* src, void* const* dst, const int* scale, int L, int C,
+                                int H, int W, int dtype, void* stream);
+
 /* A-CORR-BWD.  Replaces cuda_corr.backward (correlation.cpp:58,
    correlation_kernel.cu:275-325 + corr_backward_kernel :178-229).
    grad [B,M,2R+1,2R+1,H,W] float32.  fmap1_grad / fmap2_grad are ZEROED by
@@ -112,6 +121,13 @@ int dpvo_patchify_backward(const void* grad, const float* coords, int B, int C, 
 
 /* Workspace for dpvo_ba_forward / the split BA entry points. */
 size_t dpvo_ba_workspace_bytes(int E, int t0, int t1);
+
+/* Instrumentation / testing: which F-BA implementation dpvo_ba_forward uses.
+   0 = auto: one persistent workgroup per lower 6x6 block of S (ba_blocks.hip)
+   for E <= 2048 edges and N <= 16 free poses, the multi-kernel path (ba.hip)
+   otherwise; 1 = the single-workgroup kernel (ba_fused.hip, E <= 2048,
+   N <= 12); 2 = always the multi-kernel path; 3 = same as 0.  Process-wide. */
+int dpvo_ba_select_path(int mode);
 
 /* Largest number of free poses (t1 - t0) the single-workgroup Schur solve
    handles in this build. */

@@ -23,6 +23,16 @@ def cb(gpu):
     return dpvo_amd.load_extension("cuda_ba")
 
 
+@pytest.fixture(params=[0, 1, 2], ids=["blocks", "fused", "multikernel"])
+def path(request, cb):
+    """F-BA implementation under test: 0 = auto (one persistent workgroup per
+    block of S for these window sizes), 1 = the single-workgroup kernel,
+    2 = the multi-kernel path."""
+    cb.select_path(request.param)
+    yield request.param
+    cb.select_path(0)
+
+
 def _dev(G, gpu):
     return G.to(gpu)
 
@@ -49,7 +59,7 @@ def _check(P, K, Pr, Kr):
 
 
 @pytest.mark.parametrize("cfg,iters", [("cfg1", 1), ("cfg1", 2), ("cfg2", 1), ("cfg2", 2)])
-def test_ba_matches_oracle(cb, gpu, cfg, iters):
+def test_ba_matches_oracle(cb, gpu, path, cfg, iters):
     G = synthetic.make_config(cfg, seed=1)
     t1 = G.F
     P, K = _run_gpu(cb, G, gpu, 1, t1, iters)
@@ -87,20 +97,47 @@ def test_pose_deltas_relative(cb, gpu):
 
 
 def test_ba_is_deterministic(cb, gpu):
+    # the multi-kernel path reduces in a fixed order: bit-identical reruns
+    cb.select_path(2)
+    try:
+        G = synthetic.make_config("cfg2", seed=3)
+        a = _run_gpu(cb, G, gpu, 1, G.F, 2)
+        b = _run_gpu(cb, G, gpu, 1, G.F, 2)
+    finally:
+        cb.select_path(0)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_blocks_path_is_deterministic(cb, gpu):
+    # per-block workgroups reduce in a fixed order: bit-identical reruns
     G = synthetic.make_config("cfg2", seed=3)
     a = _run_gpu(cb, G, gpu, 1, G.F, 2)
     b = _run_gpu(cb, G, gpu, 1, G.F, 2)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
-def test_eff_impl_flag_is_same_algorithm(cb, gpu):
+def test_fused_reruns_agree(cb, gpu):
+    # the single-workgroup kernel sums in fp64 with LDS atomics (order varies
+    # run to run, like the reference's fp32 atomics): reruns agree to fp32 rounding
+    cb.select_path(1)
+    G = synthetic.make_config("cfg2", seed=3)
+    a = _run_gpu(cb, G, gpu, 1, G.F, 2)
+    for _ in range(3):
+        b = _run_gpu(cb, G, gpu, 1, G.F, 2)
+        np.testing.assert_allclose(a[0], b[0], rtol=0, atol=1e-6)
+        np.testing.assert_allclose(a[1], b[1], rtol=1e-6, atol=1e-7)
+    cb.select_path(0)
+
+
+def test_eff_impl_flag_is_same_algorithm(cb, gpu, path):
     G = synthetic.make_config("cfg1", seed=4)
     a = _run_gpu(cb, G, gpu, 1, G.F, 2, eff=False)
     b = _run_gpu(cb, G, gpu, 1, G.F, 2, eff=True)
-    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    np.testing.assert_allclose(a[0], b[0], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-6, atol=1e-7)
 
 
-def test_structure_only(cb, gpu):
+def test_structure_only(cb, gpu, path):
     # t1 == t0: dZ = Q u, poses untouched (ba_cuda.cu:521-531)
     G = synthetic.make_config("cfg1", seed=5)
     P, K = _run_gpu(cb, G, gpu, 3, 3, 2)
@@ -109,7 +146,7 @@ def test_structure_only(cb, gpu):
     np.testing.assert_array_equal(P, G.poses.numpy())
 
 
-def test_window_with_fixed_poses_and_buffers(cb, gpu):
+def test_window_with_fixed_poses_and_buffers(cb, gpu, path):
     # optimisation window t0=4 (poses < t0 fixed) inside larger pose/patch buffers
     G = synthetic.make_config("cfg2", seed=6, num_poses=64, num_patches=12 * 96 + 500)
     P, K = _run_gpu(cb, G, gpu, 4, 12, 2)
@@ -119,7 +156,7 @@ def test_window_with_fixed_poses_and_buffers(cb, gpu):
     np.testing.assert_array_equal(P[12:], G.poses.numpy()[12:])
 
 
-def test_unsorted_edges_and_shuffled_kk(cb, gpu):
+def test_unsorted_edges_and_shuffled_kk(cb, gpu, path):
     G = synthetic.make_config("cfg1", seed=7)
     perm = torch.randperm(G.E, generator=torch.Generator().manual_seed(0))
     for k in ("ii", "jj", "kk", "target", "weight"):
@@ -196,3 +233,26 @@ def test_fastba_python_surface(gpu):
               D.ii, D.jj, D.kk, 1, G.F, M=G.M, iterations=2, eff_impl=False)
     Pr, Kr = _run_oracle(G, 1, G.F, 2)
     _check(poses.cpu().numpy(), patches.cpu().numpy(), Pr, Kr)
+
+
+@pytest.mark.parametrize("seed", [20, 21])
+def test_fused_general_graph_structure(cb, gpu, path, seed):
+    """Edges whose source pose differs inside one patch, duplicate (kk, jj)
+    edges, self edges (ii == jj) and edges touching fixed poses on both sides:
+    every E-entry branch of the fused Schur assembly (prim merge, non-prim
+    source entries, cross terms) against the oracle."""
+    G = synthetic.make_config("cfg1", seed=seed)
+    r = np.random.default_rng(seed)
+    ii, jj, kk = G.ii.numpy().copy(), G.jj.numpy().copy(), G.kk.numpy().copy()
+    E = len(ii)
+    sel = r.choice(E, E // 8, replace=False)
+    ii[sel] = r.integers(0, G.F, len(sel))          # mixed source poses per patch
+    dup = r.choice(E, E // 16, replace=False)
+    ii = np.concatenate([ii, ii[dup]]); jj = np.concatenate([jj, jj[dup]])  # duplicates
+    kk = np.concatenate([kk, kk[dup]])
+    tg = torch.cat([G.target, G.target[dup] + 0.3]); wt = torch.cat([G.weight, G.weight[dup]])
+    G.ii, G.jj, G.kk = (torch.from_numpy(x).long() for x in (ii, jj, kk))
+    G.target, G.weight = tg.contiguous(), wt.contiguous()
+    P, K = _run_gpu(cb, G, gpu, 2, G.F - 1, 2)
+    Pr, Kr = _run_oracle(G, 2, G.F - 1, 2)
+    _check(P, K, Pr, Kr)

@@ -234,3 +234,21 @@ def test_to_channels_last_frame_slot(gpu):
     assert torch.count_nonzero(dst[0, :3]) == 0
     full = altcorr.to_channels_last(src)
     assert torch.equal(full, src) and full.permute(0, 1, 3, 4, 2).is_contiguous()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,scales", [(120, 160, (1, 2, 4, 8)), (120, 188, (1, 4)),
+                                        (37, 45, (1, 2, 4, 8))])
+def test_insert_frame_matches_avg_pool(gpu, H, W, scales):
+    """One-launch pyramid insertion == avg_pool2d + channels-last copy, bit-exact,
+    written only into the addressed ring slot (EuRoC 120x188 and ragged sizes)."""
+    from dpvo_amd import altcorr, synthetic
+
+    fmap = torch.randn(128, H, W, device=gpu)
+    pyr = [synthetic.channels_last(torch.full((1, 4, 128, H // s, W // s), 7.0, device=gpu))
+           for s in scales]
+    altcorr.insert_frame(fmap, pyr, 2, scales)
+    for p, s in zip(pyr, scales):
+        ref = fmap if s == 1 else torch.nn.functional.avg_pool2d(fmap[None], s, s)[0]
+        assert torch.equal(p[0, 2], ref), s
+        assert bool((p[0, [0, 1, 3]] == 7.0).all())
