@@ -3,9 +3,12 @@ synthetic patch graph -- 96 patches x 2048 edges, p=3, 4-level pyramid
 [1,2,4,8], fp32 -- on N MI355X GPUs (replicas; one process per GPU).
 
 One step = one DPVO update iteration with all inputs resident in HBM:
+  frame     insertion of one new frame into the channels-last pyramid ring
   F-REPROJ  (cuda_ba.reproject, E x 9 points)
   A-CORR    (all 4 levels in one launch, cuda_corr.forward_levels)
   F-BA      (cuda_ba.forward, 2 iterations, poses/patches updated in place)
+By default the step is captured once as a hipGraph and replayed (--eager:
+launch from Python every step).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -71,6 +74,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every kernel from Python each step (default: replay the "
+                         "step as one captured hipGraph)")
     args = ap.parse_args()
 
     import torch
@@ -110,40 +116,66 @@ def main():
     jj1 = D.jj % args.mem
     scales = [float(s) for s in levels]
 
-    ev_corr = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)]
-
-    def step(i=None):
-        slot = (i or 0) % args.mem  # frame insertion (dpvo.py:__call__ -> ring buffer)
+    def step(i=0, ev=None):
+        slot = i % args.mem  # frame insertion (dpvo.py:__call__ -> ring buffer)
         altcorr.insert_frame(pyr_nchw[0][0, slot], pyr, slot, levels)
         coords = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk)
-        if i is not None:
-            ev_corr[i][0].record()
+        if ev is not None:
+            ev[0].record()
         corr = altcorr.corr_levels(gbuf, pyr, coords, kk1, jj1, 3, scales)
-        if i is not None:
-            ev_corr[i][1].record()
+        if ev is not None:
+            ev[1].record()
         fastba.BA(poses, patches, D.intrinsics, D.target, D.weight, lmbda, D.ii, D.jj, D.kk, 1,
                   G.F, M=G.M, iterations=args.ba_iters)
         return corr
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize()
+    # A-CORR kernel time for the roofline: HIP events around the corr launch
+    # (same stream) over eager steps outside the timed region
+    n_ev = 20
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(n_ev)]
+    for i in range(n_ev):
+        step(i, evs[i])
+    torch.cuda.synchronize()
+    corr_ms = sorted(a.elapsed_time(b) for a, b in evs)[n_ev // 2]
     coords0 = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk)
     alg_bytes, per_level = algorithmic_corr_bytes(
         coords0, [f.shape[3] for f in pyr], [f.shape[4] for f in pyr], scales, C, P, 3, 4)
+
+    graph = None
+    if not args.eager:
+        # one update iteration (frame insertion, reproject, corr, 2 BA iterations)
+        # captured once and replayed: the same kernels with the same work, without
+        # the per-launch Python / runtime gaps
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for i in range(3):
+                step(i)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step(0)
+        graph.replay()
+        torch.cuda.synchronize()
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        if graph is not None:
+            graph.replay()
+        else:
+            step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    corr_ms = sum(a.elapsed_time(b) for a, b in ev_corr) / args.steps
 
     if world > 1:
         t = torch.tensor([elapsed, corr_ms], device=dev, dtype=torch.float64)
@@ -180,6 +212,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (SURVEY 8d cfg2 recipe, seeded)",
+            "launch": "eager" if graph is None else "hipGraph replay of one captured step",
             "config": {
                 "workload": f"{args.config}: {G.M} patches/frame x {G.E} edges, p={P}, "
                             f"{len(levels)}-level pyramid {levels}, fp32, BA {args.ba_iters} iters",

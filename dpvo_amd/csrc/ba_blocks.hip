@@ -33,6 +33,10 @@
 //   All spin-waits carry a wall-clock timeout so the grid always drains.
 // The grid (<= 136 workgroups of 512 threads) is far below one workgroup per
 // CU, so all workgroups are co-resident.
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "ba_device.hpp"
 
 namespace dpvo {
@@ -50,6 +54,7 @@ constexpr unsigned kGlb = 0xFE;     // pose slot: read from HBM
 constexpr int kV = 42;              // per-thread block accumulators: 36 S + 6 y
 constexpr int kRedCols = 128;
 constexpr long long kSpinTicks = 2000000;  // 20 ms of the 100 MHz wall clock
+constexpr int kEpochWord = 2 * (kBMaxN * (kBMaxN + 1) / 2) + 4;  // in the flag buffer
 
 struct BArgs {
   float* poses;
@@ -65,7 +70,8 @@ struct BArgs {
   double* Sg;      // [NB][2][36] the two halves of every block of S
   double* yg;      // [2][6N]
   double* dXg;     // [2][6N] dX of iteration it in slot it & 1
-  int* sync;       // [4]: arrivals (NB per iteration), iterations done, timeout flag
+  long long* flags;  // persistent [G + 1]: arrival of workgroup g, [G] dX published
+  long long epoch;   // unused on the host side (read on the device from flags[kEpochWord])
   double* EW;      // [2 NB][E][12] entries e_j, e_i of each relevant edge (per workgroup)
   double* QU;      // [NB][E][2]  Q, u of each relevant patch
   int* gidx;       // [NB][E][2]  pose indices of relevant edges (slot kGlb)
@@ -98,8 +104,8 @@ __device__ __forceinline__ unsigned code_of(unsigned slot, int N) {
   return slot < (unsigned)N ? slot : kFixed;
 }
 
-// spin (thread 0) until *p >= target; returns false on timeout
-__device__ bool wait_geq(int* p, int target) {
+// spin until *p >= target; returns false on timeout
+__device__ bool wait_geq(long long* p, long long target) {
   const long long t0 = (long long)wall_clock64();
   while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
     __builtin_amdgcn_s_sleep(1);
@@ -159,34 +165,44 @@ __device__ void block_ldl_solve(const Solver& L, int N, double* dX, int* fail, i
     __syncthreads();
     if (m == 0) break;
     const int ntask = 6 * (m * (m + 1) / 2);
-    // task t = 6 * bt + x, bt in lower-triangle order of the trailing blocks;
-    // tasks 0..5 are the rows of block (k+1, k+1)
-    const int tb = (wid == 0) ? lane : 6 + (tid - 64);
-    const int ts = (wid == 0) ? 64 : T - 64;
-    const int tend = (wid == 0) ? 6 : ntask;
-    for (int t = tb; t < tend; t += ts) {
-      const int x = t % 6;
-      int a, b;
-      tri_of(t / 6, a, b);
-      const int i = k + 1 + a, j = k + 1 + b;
-      const double* Vi = L.PV + 36 * i + 6 * x;
-      const double* Wj = L.S + 36 * lblk(j, k);
-      double* Sij = L.S + 36 * lblk(i, j) + 6 * x;
-      double v[6], w[36];
+    if (wid == 0) {
+      // look-ahead: pivot block (k+1, k+1), one entry per lane (36 lanes)
+      if (lane < 36) {
+        const int x = lane / 6, z = lane % 6, i = k + 1;
+        const double* Vi = L.PV + 36 * i + 6 * x;
+        const double* Wz = L.S + 36 * lblk(i, k) + 6 * z;
+        double* Sxz = L.S + 36 * lblk(i, i) + 6 * x + z;
+        double s = *Sxz;
 #pragma unroll
-      for (int q = 0; q < 6; q++) v[q] = Vi[q];
-#pragma unroll
-      for (int q = 0; q < 36; q += 2) {
-        const double2 p2 = *reinterpret_cast<const double2*>(Wj + q);
-        w[q] = p2.x;
-        w[q + 1] = p2.y;
+        for (int q = 0; q < 6; q++) s -= Vi[q] * Wz[q];
+        *Sxz = s;
       }
+    } else {
+      // tasks 6.. (rows of the other trailing blocks) on waves 1..
+      for (int t = 6 + (tid - 64); t < ntask; t += T - 64) {
+        const int x = t % 6;
+        int a, b;
+        tri_of(t / 6, a, b);
+        const int i = k + 1 + a, j = k + 1 + b;
+        const double* Vi = L.PV + 36 * i + 6 * x;
+        const double* Wj = L.S + 36 * lblk(j, k);
+        double* Sij = L.S + 36 * lblk(i, j) + 6 * x;
+        double v[6], w[36];
 #pragma unroll
-      for (int z = 0; z < 6; z++) {  // diagonal blocks stay full (symmetric)
-        double s = Sij[z];
+        for (int q = 0; q < 6; q++) v[q] = Vi[q];
 #pragma unroll
-        for (int q = 0; q < 6; q++) s -= v[q] * w[6 * z + q];
-        Sij[z] = s;
+        for (int q = 0; q < 36; q += 2) {
+          const double2 p2 = *reinterpret_cast<const double2*>(Wj + q);
+          w[q] = p2.x;
+          w[q + 1] = p2.y;
+        }
+#pragma unroll
+        for (int z = 0; z < 6; z++) {  // diagonal blocks stay full (symmetric)
+          double s = Sij[z];
+#pragma unroll
+          for (int q = 0; q < 6; q++) s -= v[q] * w[6 * z + q];
+          Sij[z] = s;
+        }
       }
     }
     if (wid == 0) {
@@ -492,7 +508,8 @@ __device__ void assemble(const Ctx& c) {
   __syncthreads();
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    atomicAdd(&A.sync[0], 1);
+    __hip_atomic_store(&A.flags[c.g], A.epoch * 64 + c.it + 1, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -512,6 +529,11 @@ __global__ void __launch_bounds__(kBT) ba_blocks_kernel(BArgs A) {
   const float fx = A.intrinsics[0], fy = A.intrinsics[1], cx = A.intrinsics[2],
               cy = A.intrinsics[3];
   const int kmaxc = A.num_patches - 1;
+  // this call's tag: read by every workgroup at start, advanced by workgroup 0
+  // at its very end (after every workgroup has read it: they all arrive in
+  // iteration 0 first), so graph replays get fresh tags too
+  BArgs& Am = const_cast<BArgs&>(A);
+  Am.epoch = __hip_atomic_load(&A.flags[kEpochWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   double* EW = A.EW + (size_t)g * E * 12;
   double* QU = A.QU + (size_t)g * E * 2;
   int* gidx = A.gidx + (size_t)g * E * 2;
@@ -815,7 +837,7 @@ __global__ void __launch_bounds__(kBT) ba_blocks_kernel(BArgs A) {
   // inverse depths of the relevant patches (entries / Q, u of iteration it)
   auto apply_step = [&](int it) {
     if (tid == 0) {
-      if (!wait_geq(&A.sync[1], it + 1)) ctl[kCTimeout] = 1;
+      if (!wait_geq(&A.flags[gridDim.x], A.epoch * 64 + it + 1)) ctl[kCTimeout] = 1;
     }
     __syncthreads();
     const double* dXi = A.dXg + (size_t)(it & 1) * 6 * N;
@@ -907,9 +929,8 @@ __global__ void __launch_bounds__(kBT) ba_blocks_kernel(BArgs A) {
       sv.PV = sv.tt + 6 * NN;
       double* dXo = A.dXg + (size_t)(it & 1) * 6 * N;
       if (NB > 0) {
-        if (tid == 0) {
-          if (!wait_geq(&A.sync[0], 2 * NB * (it + 1))) ctl[kCTimeout] = 1;
-        }
+        for (int w = tid; w < 2 * NB; w += T)  // one lane per arrival flag
+          if (!wait_geq(&A.flags[w], A.epoch * 64 + it + 1)) ctl[kCTimeout] = 1;
         __syncthreads();
         bstamp(A, mb + 2);
         {  // sum the two halves of every block (fixed order); 8 loads in flight
@@ -946,7 +967,8 @@ __global__ void __launch_bounds__(kBT) ba_blocks_kernel(BArgs A) {
       bstamp(A, mb + 6);
       if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_store(&A.sync[1], it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&A.flags[gridDim.x], A.epoch * 64 + it + 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -964,12 +986,12 @@ __global__ void __launch_bounds__(kBT) ba_blocks_kernel(BArgs A) {
         for (int c = 0; c < 7; c++) A.poses[7 * (size_t)gp + c] = L.pose[8 * i + c];
     }
     if (tid == 0) {
+      __hip_atomic_store(&A.flags[kEpochWord], A.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       A.meta[0] = nuniq;
       A.meta[1] = (ctl[kCFail] ? 1 : 0) | (ctl[kCBad] ? 2 : 0) | (ctl[kCTimeout] ? 16 : 0);
     }
     bstamp(A, 63);
   }
-  if (tid == 0 && ctl[kCTimeout]) atomicOr(&A.sync[2], 1);
   (void)timeout;
 }
 
@@ -981,14 +1003,38 @@ static size_t al256(size_t v) { return (v + 255) / 256 * 256; }
 size_t ba_blocks_scratch_bytes(int E, int N) {
   const int NB = N * (N + 1) / 2, G = NB > 0 ? 2 * NB : 1, N1 = N > 0 ? N : 1;
   return al256(sizeof(double) * 36 * G) + al256(sizeof(double) * 12 * N1) +
-         al256(sizeof(double) * 12 * N1) + al256(sizeof(int) * 4) +
-         al256(sizeof(double) * 12 * (size_t)G * E) + al256(sizeof(double) * 2 * (size_t)G * E) +
-         al256(sizeof(int) * 2 * (size_t)G * E) + al256(sizeof(int) * (size_t)G * E) +
-         al256(sizeof(float) * (size_t)G * E);
+         al256(sizeof(double) * 12 * N1) + al256(sizeof(double) * 12 * (size_t)G * E) +
+         al256(sizeof(double) * 2 * (size_t)G * E) + al256(sizeof(int) * 2 * (size_t)G * E) +
+         al256(sizeof(int) * (size_t)G * E) + al256(sizeof(float) * (size_t)G * E);
 }
 
 bool ba_blocks_supported(int E, int N, int P) {
   return E > 0 && E <= kBMaxE && N >= 0 && N <= kBMaxN && P >= 2 && P * P <= 64;
+}
+
+// Arrival / publish flags live in library-owned device memory, one set per
+// device, zeroed once (so a hipGraph capture on a side stream finds them
+// allocated; BA calls on one device must therefore not overlap in time).  Every call tags its flags with a new epoch
+// kept in the same buffer (advanced on the device), so no per-call reset
+// (memset launch) is needed, a call that timed out cannot confuse the next
+// one, and hipGraph replays stay correct.
+namespace {
+constexpr int kFlagWords = 2 * (kBMaxN * (kBMaxN + 1) / 2) + 8;
+std::mutex g_flag_mu;
+std::map<int, long long*> g_flags;  // per device (streams share it: see below)
+}  // namespace
+
+static long long* flag_slot(hipStream_t st) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_flag_mu);
+  auto it = g_flags.find(dev);
+  if (it != g_flags.end()) return it->second;
+  long long* p = nullptr;
+  if (hipMalloc(&p, sizeof(long long) * kFlagWords) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, sizeof(long long) * kFlagWords, st) != hipSuccess) return nullptr;
+  g_flags[dev] = p;
+  return p;
 }
 
 int ba_blocks_launch(float* poses, float* patches, const float* intrinsics, const float* target,
@@ -1001,8 +1047,13 @@ int ba_blocks_launch(float* poses, float* patches, const float* intrinsics, cons
                               hipFuncAttributeMaxDynamicSharedMemorySize, kBLds);
     attr = true;
   }
+  if (iterations > 63) return DPVO_ERR_UNSUPPORTED;  // 6-bit iteration tag per epoch
   const int N = t1 - t0, NB = N * (N + 1) / 2, G = NB > 0 ? 2 * NB : 1, N1 = N > 0 ? N : 1;
+  hipStream_t st = as_stream(stream);
   BArgs a;
+  a.flags = flag_slot(st);
+  a.epoch = 0;
+  if (!a.flags) return DPVO_ERR_LAUNCH;
   a.poses = poses;
   a.patches = patches;
   a.intrinsics = intrinsics;
@@ -1027,8 +1078,6 @@ int ba_blocks_launch(float* poses, float* patches, const float* intrinsics, cons
   s += al256(sizeof(double) * 12 * N1);
   a.dXg = (double*)s;
   s += al256(sizeof(double) * 12 * N1);
-  a.sync = (int*)s;
-  s += al256(sizeof(int) * 4);
   a.EW = (double*)s;
   s += al256(sizeof(double) * 12 * (size_t)G * E);
   a.QU = (double*)s;
@@ -1040,8 +1089,6 @@ int ba_blocks_launch(float* poses, float* patches, const float* intrinsics, cons
   a.dbw = (float*)s;
   a.meta = meta;
   a.marks = marks;
-  hipStream_t st = as_stream(stream);
-  if (hipMemsetAsync(a.sync, 0, sizeof(int) * 4, st) != hipSuccess) return DPVO_ERR_LAUNCH;
   hipLaunchKernelGGL(ba_blocks_kernel, dim3(G), dim3(kBT), kBLds, st, a);
   return launch_status();
 }

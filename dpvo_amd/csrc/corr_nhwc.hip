@@ -255,43 +255,103 @@ struct InsLevels {
   int s[kMaxL];
 };
 
+// level-1 copy of the LDS tile: one float4 (4 channels) per lane, 8 lanes per
+// pixel = one 128-B run of the channels-last row
+__device__ __forceinline__ void ins_copy(const float* tile, float* dstl, int tx0, int ty0,
+                                         int c0, int C, int H, int W, int tid) {
+  for (int it = tid; it < kInsTY * kInsTX * 8; it += 256) {
+    const int cg = it & 7, q = it >> 3, py = q / kInsTX, px = q % kInsTX;
+    const int oy = ty0 + py, ox = tx0 + px, gc = c0 + 4 * cg;
+    if (oy >= H || ox >= W || gc >= C) continue;
+    const float* t = tile + (4 * cg) * kInsCS + py * kInsTX + px;
+    float* dst = dstl + ((size_t)oy * W + ox) * C + gc;
+    if (gc + 4 <= C && (C & 3) == 0) {
+      *reinterpret_cast<float4*>(dst) =
+          make_float4(t[0], t[kInsCS], t[2 * kInsCS], t[3 * kInsCS]);
+    } else {
+      for (int k = 0; k < 4 && gc + k < C; k++) dst[k] = t[k * kInsCS];
+    }
+  }
+}
+
+// pooled level S (avg_pool2d kernel = stride = S): one channel per lane, 32
+// lanes per pixel (a 128-B run); the S*S window is summed in avg_pool2d's
+// row-major order and divided by S^2, fully unrolled so the LDS reads issue
+// back to back (bit-exact with torch)
+template <int S>
+__device__ __forceinline__ void ins_pool(const float* tile, float* dstl, int tx0, int ty0,
+                                         int c0, int C, int H, int W, int tid) {
+  constexpr int nty = kInsTY / S, ntx = kInsTX / S;
+  const int Hs = H / S, Ws = W / S, oy0 = ty0 / S, ox0 = tx0 / S;
+  for (int it = tid; it < nty * ntx * kInsTC; it += 256) {
+    const int c = it & (kInsTC - 1), q = it / kInsTC, py = q / ntx, px = q % ntx;
+    const int oy = oy0 + py, ox = ox0 + px, gc = c0 + c;
+    if (oy >= Hs || ox >= Ws || gc >= C) continue;
+    const float* t = tile + c * kInsCS + py * S * kInsTX + px * S;
+    float w[S * S];
+#pragma unroll
+    for (int a = 0; a < S; a++)
+#pragma unroll
+      for (int b = 0; b < S; b++) w[a * S + b] = t[a * kInsTX + b];
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < S * S; k++) acc += w[k];
+    dstl[((size_t)oy * Ws + ox) * C + gc] = acc / (float)(S * S);
+  }
+}
+
 __global__ void __launch_bounds__(256)
     pyramid_insert_kernel(const float* __restrict__ src, InsLevels lv, int L, int C, int H,
                           int W) {
   __shared__ float tile[kInsTC * kInsCS];
   const int tx0 = blockIdx.x * kInsTX, ty0 = blockIdx.y * kInsTY, c0 = blockIdx.z * kInsTC;
   const int tid = threadIdx.x;
-  // load: 32 channels x 8 rows x 32 px (one 128-B row per 32 lanes)
-#pragma unroll 4
-  for (int k = tid; k < kInsTC * kInsTY * kInsTX; k += 256) {
-    const int x = k & 31, y = (k >> 5) & 7, c = k >> 8;
-    const int gx = tx0 + x, gy = ty0 + y, gc = c0 + c;
-    float v = 0.0f;
-    if (gx < W && gy < H && gc < C) v = src[((size_t)gc * H + gy) * W + gx];
-    tile[c * kInsCS + y * kInsTX + x] = v;
+  // load: 32 channels x 8 rows x 32 px as float4 (8 per thread, all issued
+  // before the first LDS store: one HBM latency per tile, not eight)
+  if ((W & 3) == 0) {
+    float4 v[8];
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      const int k = tid + 256 * r;  // (c, y, x4) = (k >> 6, (k >> 3) & 7, k & 7)
+      const int c = k >> 6, y = (k >> 3) & 7, x = 4 * (k & 7);
+      const int gx = tx0 + x, gy = ty0 + y, gc = c0 + c;
+      v[r] = (gx < W && gy < H && gc < C)
+                 ? *reinterpret_cast<const float4*>(src + ((size_t)gc * H + gy) * W + gx)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      const int k = tid + 256 * r;
+      const int c = k >> 6, y = (k >> 3) & 7, x = 4 * (k & 7);
+      float* t = tile + c * kInsCS + y * kInsTX + x;
+      t[0] = v[r].x;
+      t[1] = v[r].y;
+      t[2] = v[r].z;
+      t[3] = v[r].w;
+    }
+  } else {
+    float v[32];
+#pragma unroll
+    for (int r = 0; r < 32; r++) {
+      const int k = tid + 256 * r;
+      const int x = k & 31, y = (k >> 5) & 7, c = k >> 8;
+      const int gx = tx0 + x, gy = ty0 + y, gc = c0 + c;
+      v[r] = (gx < W && gy < H && gc < C) ? src[((size_t)gc * H + gy) * W + gx] : 0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < 32; r++) {
+      const int k = tid + 256 * r;
+      tile[(k >> 8) * kInsCS + ((k >> 5) & 7) * kInsTX + (k & 31)] = v[r];
+    }
   }
   __syncthreads();
-  const int lane_c = tid & 31, grp = tid >> 5;  // 8 pixel groups of 32 channel lanes
-  const int gc = c0 + lane_c;
+  // level 1: one float4 (4 channels) per lane, 8 lanes per pixel = one 128-B run
   for (int l = 0; l < L; l++) {
-    const int s = lv.s[l];
-    const int Hs = H / s, Ws = W / s;
-    const int oy0 = ty0 / s, ox0 = tx0 / s, nty = kInsTY / s, ntx = kInsTX / s;
-    const float inv = (float)(s * s);
-    for (int q = grp; q < nty * ntx; q += 8) {
-      const int oy = oy0 + q / ntx, ox = ox0 + q % ntx;
-      if (oy >= Hs || ox >= Ws || gc >= C) continue;
-      const float* t = tile + lane_c * kInsCS + (q / ntx) * s * kInsTX + (q % ntx) * s;
-      float v;
-      if (s == 1) {
-        v = t[0];
-      } else {
-        float acc = 0.0f;
-        for (int a = 0; a < s; a++)
-          for (int b = 0; b < s; b++) acc += t[a * kInsTX + b];
-        v = acc / inv;
-      }
-      lv.dst[l][((size_t)oy * Ws + ox) * C + gc] = v;
+    switch (lv.s[l]) {
+      case 1: ins_copy(tile, lv.dst[l], tx0, ty0, c0, C, H, W, tid); break;
+      case 2: ins_pool<2>(tile, lv.dst[l], tx0, ty0, c0, C, H, W, tid); break;
+      case 4: ins_pool<4>(tile, lv.dst[l], tx0, ty0, c0, C, H, W, tid); break;
+      default: ins_pool<8>(tile, lv.dst[l], tx0, ty0, c0, C, H, W, tid); break;
     }
   }
 }
