@@ -30,7 +30,7 @@ INCLUDE = os.path.join(REPO, "include")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("DPVO_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["corr.hip", "corr_nhwc.hip", "ba.hip", "ba_fused.hip", "ba_blocks.hip", "lie.hip"]
+HIP_SOURCES = ["corr.hip", "corr_nhwc.hip", "ba.hip", "ba_fused.hip", "ba_blocks.hip", "ba_large.hip", "lie.hip"]
 EXTENSIONS = {
     "cuda_corr": "ext_cuda_corr.cpp",
     "cuda_ba": "ext_cuda_ba.cpp",
@@ -77,10 +77,20 @@ def build(force=False, verbose=False):
     hdr = [os.path.join(INCLUDE, "dpvo_hot.h")] + [os.path.join(CSRC, h) for h in HEADERS]
     lib = lib_path()
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
-    if force or _stale(lib, srcs + hdr + [__file__]):
-        cmd = [hipcc, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared",
-               "-fvisibility=hidden", "-mcode-object-version=5", "-Wno-unused-result",
-               f"-I{INCLUDE}", f'-DDPVO_GIT_REV="{_git_rev()}"', *srcs, "-o", lib]
+    # one object per HIP source (incremental), then one shared library
+    objdir = os.path.join(OUT, "obj")
+    os.makedirs(objdir, exist_ok=True)
+    objs = []
+    for src in srcs:
+        obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
+        objs.append(obj)
+        if force or _stale(obj, [src] + hdr + [__file__]):
+            cmd = [hipcc, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c",
+                   "-fvisibility=hidden", "-mcode-object-version=5", "-Wno-unused-result",
+                   f"-I{INCLUDE}", f'-DDPVO_GIT_REV="{_git_rev()}"', src, "-o", obj]
+            _run(cmd, verbose)
+    if force or _stale(lib, objs):
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-o", lib]
         _run(cmd, verbose)
 
     import torch

@@ -1070,11 +1070,18 @@ int ba_blocks_launch(float* poses, float* patches, const float* intrinsics, cons
                      const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                      const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
                      int iterations, char* scratch, int* meta, int64_t* marks, void* stream);
+// ba_large.hip: large graphs (global BA, cfg4)
+size_t gba_workspace_bytes(int E, int N);
+int gba_forward(float* poses, float* patches, const float* intrinsics, const float* target,
+                const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
+                const int64_t* kk, int E, int P, int num_poses, int num_patches, int PPF, int t0,
+                int t1, int iterations, void* workspace, size_t workspace_bytes, void* stream);
 
 }  // namespace dpvo
 
 namespace {
-int g_ba_path = 0;  // 0 auto (blocks), 1 fused single workgroup, 2 multi-kernel, 3 blocks
+// 0 auto (blocks), 1 fused single workgroup, 2 multi-kernel, 3 blocks, 4 large-graph path
+int g_ba_path = 0;
 }
 
 using namespace dpvo;
@@ -1124,20 +1131,33 @@ static BaArgs make_args(float* poses, float* patches, const float* intrinsics, c
 static int schur_grid(int N) { return N * (N + 1) / 2; }
 static int lin_grid(int E) { return (E + 255) / 256; }
 
+// the window paths (blocks / fused / multi-kernel) cover E <= kMaxSetupE and
+// N <= kMaxFree; anything larger (global BA, cfg4) runs ba_large.hip
+static bool window_path_ok(int E, int N) { return E <= kMaxSetupE && N <= kMaxFree; }
+static bool use_large(int E, int N) { return g_ba_path == 4 || !window_path_ok(E, N); }
+
 DPVO_EXPORT size_t dpvo_ba_workspace_bytes(int E, int t0, int t1) {
   const int N = t1 > t0 ? t1 - t0 : 0;
   const int Ep = E > 0 ? E : 1;
-  const size_t a = ba_fused_scratch_bytes(Ep, N), b = ba_blocks_scratch_bytes(Ep, N);
-  return ba_layout(Ep, N, nullptr, nullptr) + (a > b ? a : b);
+  size_t bytes = 0;
+  if (window_path_ok(Ep, N)) {
+    const size_t a = ba_fused_scratch_bytes(Ep, N), b = ba_blocks_scratch_bytes(Ep, N);
+    bytes = ba_layout(Ep, N, nullptr, nullptr) + (a > b ? a : b);
+  }
+  if (use_large(Ep, N)) {
+    const size_t g = gba_workspace_bytes(Ep, N);
+    bytes = g > bytes ? g : bytes;
+  }
+  return bytes;
 }
 
 DPVO_EXPORT int dpvo_ba_select_path(int mode) {
-  if (mode < 0 || mode > 3) return DPVO_ERR_INVALID;
+  if (mode < 0 || mode > 4) return DPVO_ERR_INVALID;
   g_ba_path = mode;
   return DPVO_OK;
 }
 
-DPVO_EXPORT int dpvo_ba_max_free_poses(void) { return kMaxFree; }
+DPVO_EXPORT int dpvo_ba_max_free_poses(void) { return dpvo_gba_max_free_poses(); }
 
 DPVO_EXPORT int dpvo_ba_setup(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E,
                               int num_patches, int t0, int t1, void* workspace,
@@ -1252,8 +1272,11 @@ DPVO_EXPORT int dpvo_ba_forward(float* poses, float* patches, const float* intri
       !patches || !intrinsics || !target || !weight || !lmbda || !ii || !jj || !kk)
     return DPVO_ERR_INVALID;
   const int N = t1 - t0;
-  if (E > kMaxSetupE || N > kMaxFree) return DPVO_ERR_UNSUPPORTED;
   if (workspace_bytes < dpvo_ba_workspace_bytes(E, t0, t1)) return DPVO_ERR_WORKSPACE;
+  if (use_large(E, N))
+    return gba_forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
+                       num_poses, num_patches, PPF, t0, t1, iterations, workspace,
+                       workspace_bytes, stream);
   BaWs w;
   const size_t base_bytes = ba_layout(E, N, (char*)workspace, &w);
   if ((g_ba_path == 0 || g_ba_path == 3) && ba_blocks_supported(E, N, P))

@@ -43,8 +43,7 @@ static torch::Tensor ba_forward_ws(torch::Tensor poses, torch::Tensor patches,
   TORCH_CHECK(target.numel() >= 2 * E && weight.numel() >= 2 * E, "target/weight must be [.., E, 2]");
   if (E == 0 || iterations <= 0) return torch::Tensor();
   TORCH_CHECK(t1 - t0 <= dpvo_ba_max_free_poses(), "cuda_ba.forward: t1 - t0 = ", t1 - t0,
-              " free poses exceeds this build's single-workgroup Schur solve (",
-              dpvo_ba_max_free_poses(), ")");
+              " free poses exceeds this build's limit (", dpvo_ba_max_free_poses(), ")");
   const size_t wsb = dpvo_ba_workspace_bytes(E, t0, t1);
   auto ws = torch::empty({(int64_t)wsb}, poses.options().dtype(torch::kUInt8));
   check_status(dpvo_ba_forward(poses.data_ptr<float>(), patches.data_ptr<float>(),
@@ -207,6 +206,73 @@ torch::Tensor ba_last_status(torch::Tensor ws, int E, int t0, int t1) {
   return out;
 }
 
+// Large-graph F-BA split for the edge-sharded driver (dpvo_amd/fastba/sharded.py):
+// setup -> [build -> all_reduce(packed) -> solve_update] x iterations.
+torch::Tensor gba_setup(torch::Tensor ii, torch::Tensor jj, torch::Tensor kk, int num_patches,
+                        int PPF, int t0, int t1, int own_lo, int own_hi) {
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  kk = idx64(kk, "kk");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ii.device());
+  const int E = ii.numel();
+  TORCH_CHECK(E > 0, "gba_setup: empty graph");
+  const size_t wsb = dpvo_gba_workspace_bytes(E, t0, t1);
+  auto ws = torch::empty({(int64_t)wsb}, ii.options().dtype(torch::kUInt8));
+  check_status(dpvo_gba_setup(ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(),
+                              kk.data_ptr<int64_t>(), E, num_patches, PPF, t0, t1, own_lo, own_hi,
+                              ws.data_ptr(), wsb, current_stream()),
+               "cuda_ba.gba_setup");
+  return ws;
+}
+
+void gba_build(torch::Tensor ws, torch::Tensor poses, torch::Tensor patches,
+               torch::Tensor intrinsics, torch::Tensor target, torch::Tensor weight,
+               torch::Tensor lmbda, torch::Tensor ii, torch::Tensor jj, int t0, int t1) {
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  TORCH_CHECK(poses.is_contiguous() && patches.is_contiguous(), "poses/patches contiguous");
+  poses = f32_contig(poses, "poses");
+  patches = f32_contig(patches, "patches");
+  intrinsics = f32_contig(intrinsics, "intrinsics");
+  target = f32_contig(target, "target");
+  weight = f32_contig(weight, "weight");
+  lmbda = f32_contig(lmbda, "lmbda");
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  const int E = ii.numel(), P = patches.size(-1);
+  TORCH_CHECK(ws.numel() >= (int64_t)dpvo_gba_workspace_bytes(E, t0, t1), "workspace too small");
+  check_status(dpvo_gba_build(poses.data_ptr<float>(), patches.data_ptr<float>(),
+                              intrinsics.data_ptr<float>(), target.data_ptr<float>(),
+                              weight.data_ptr<float>(), lmbda.data_ptr<float>(),
+                              ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), E, P,
+                              poses.numel() / 7, t0, t1, ws.data_ptr(), current_stream()),
+               "cuda_ba.gba_build");
+}
+
+// the packed [y (6N) | S blocks (nblk x 36)] fp64 system inside the workspace
+torch::Tensor gba_packed(torch::Tensor ws, int E, int t0, int t1, int64_t nblk) {
+  const int64_t N = t1 > t0 ? t1 - t0 : 0;
+  const int64_t off = (int64_t)dpvo_gba_packed_offset(E, t0, t1);
+  const int64_t n = 6 * N + 36 * nblk;
+  TORCH_CHECK(off % 8 == 0 && off + 8 * n <= ws.numel(), "gba_packed: bad extent");
+  return ws.narrow(0, off, 8 * n).view(torch::kFloat64);
+}
+
+void gba_solve_update(torch::Tensor ws, torch::Tensor poses, torch::Tensor patches, int E, int t0,
+                      int t1) {
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  TORCH_CHECK(poses.is_contiguous() && patches.is_contiguous(), "poses/patches contiguous");
+  check_status(dpvo_gba_solve_update(poses.data_ptr<float>(), patches.data_ptr<float>(), E,
+                                     patches.size(-1), t0, t1, ws.data_ptr(), current_stream()),
+               "cuda_ba.gba_solve_update");
+}
+
+torch::Tensor gba_info(torch::Tensor ws, int E, int t0, int t1) {
+  auto out = torch::zeros({8}, ws.options().dtype(torch::kInt32));
+  check_status(dpvo_gba_info(ws.data_ptr(), E, t0, t1, out.data_ptr<int>(), current_stream()),
+               "cuda_ba.gba_info");
+  return out;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("forward", &ba_forward, "BA forward operator");
   m.def("neighbors", &ba_neighbors, "temporal neighboor indicies");
@@ -218,8 +284,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("solve_update", &ba_solve_update, "Cholesky solve + pose/patch retraction");
   m.def("last_status", &ba_last_status, "status word of the last BA on a workspace");
   m.def("max_free_poses", &dpvo_ba_max_free_poses);
+  m.def("gba_setup", &gba_setup, "large-graph BA setup (ownership own_lo <= kk/PPF < own_hi)");
+  m.def("gba_build", &gba_build, "large-graph BA: linearise owned patches -> packed (y, S)");
+  m.def("gba_packed", &gba_packed, "view of the packed fp64 [y | S blocks] system");
+  m.def("gba_solve_update", &gba_solve_update, "large-graph BA: solve + retraction");
+  m.def("gba_info", &gba_info, "status, nuniq, nitems, nblk, nI, nB, g, nsb (device int32[8])");
   m.def("forward_marks", &ba_forward_marks, "forward + per-phase wall-clock marks");
   m.def("select_path", [](int mode) { check_status(dpvo_ba_select_path(mode), "select_path"); },
-        "F-BA implementation: 0 auto (fused single-workgroup where supported), 2 multi-kernel");
+        "F-BA implementation: 0 auto, 1 fused single workgroup, 2 multi-kernel, 3 blocks, 4 large-graph");
   m.attr("native_library") = dpvo_version();
 }

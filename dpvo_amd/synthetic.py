@@ -5,6 +5,7 @@ seeded torch.Generator and then copied, so every rank / run sees the same
 graph for the same seed.
 
 cfg1: F=8 frames x M=32 patches, 256 edges.   cfg2: F=12 x 96, 2048 edges.
+cfg4: F=1024 x 96, ~131k edges incl. loop blocks (make_graph_large).
 Poses Exp(xi_f), xi_f = [0, 0, 0.05 f, 0, 0, 0] + 0.01 N(0, I6); patch centres
 U([4,155] x [4,115]) at 1/4 resolution 160x120, inverse depth U(0.2, 1.2);
 edges: one per patch plus random extra ones with |j - i| <= 5, sorted by
@@ -50,21 +51,25 @@ def _qrot(q, p):
     return p + w * uv + np.cross(v, uv)
 
 
+def _qrot_n(q, p):  # batched quaternion rotation, q [n, 4] (x, y, z, w), p [n, 3]
+    v, w = q[:, :3], q[:, 3:4]
+    uv = 2 * np.cross(v, p)
+    return p + w * uv + np.cross(v, uv)
+
+
 def reproject_centres(poses, patches, intr, ii, jj, kk):
-    """Centre-pixel reprojection (fp64, host) used only to place targets."""
+    """Centre-pixel reprojection (fp64, host) used only to place targets:
+    G_ij = P_j P_i^-1 applied to the homogeneous centre point (X, d)."""
     fx, fy, cx, cy = intr
-    out = np.zeros((len(ii), 2))
-    for e, (i, j, k) in enumerate(zip(ii, jj, kk)):
-        Pi, Pj = poses[i], poses[j]
-        qi_inv = np.array([-Pi[3], -Pi[4], -Pi[5], Pi[6]])
-        # G_ij = P_j P_i^-1 applied to X: P_j (P_i^-1 X)
-        c = patches[k, :, 1, 1]
-        X = np.array([(c[0] - cx) / fx, (c[1] - cy) / fy, 1.0])
-        d = c[2]
-        Xw = _qrot(qi_inv, X - Pi[:3] * d)   # P_i^-1 applied to (X, d)
-        Xj = _qrot(Pj[3:], Xw) + Pj[:3] * d
-        out[e] = [fx * Xj[0] / Xj[2] + cx, fy * Xj[1] / Xj[2] + cy]
-    return out
+    poses = np.asarray(poses, np.float64)
+    Pi, Pj = poses[np.asarray(ii)], poses[np.asarray(jj)]
+    c = np.asarray(patches, np.float64)[np.asarray(kk), :, 1, 1]
+    X = np.stack([(c[:, 0] - cx) / fx, (c[:, 1] - cy) / fy, np.ones(len(c))], -1)
+    d = c[:, 2:3]
+    qi_inv = np.concatenate([-Pi[:, 3:6], Pi[:, 6:7]], -1)
+    Xw = _qrot_n(qi_inv, X - Pi[:, :3] * d)
+    Xj = _qrot_n(Pj[:, 3:], Xw) + Pj[:, :3] * d
+    return np.stack([fx * Xj[:, 0] / Xj[:, 2] + cx, fy * Xj[:, 1] / Xj[:, 2] + cy], -1)
 
 
 @dataclass
@@ -143,7 +148,74 @@ def make_graph(F, M, E, seed=0, H=120, W=160, p=3, span=5, noise=0.5, lateral=0.
     return Graph(poses, P, intrinsics, ii, jj, kk, target, weight, F, M)
 
 
+LARGE_CONFIGS = {
+    # BASELINE cfg4: 1024 frames x 96 patches, ~131k edges
+    "cfg4": dict(F=1024, M=96, n_random=32000, n_loops=10),
+    # same recipe at oracle-checkable sizes (tests)
+    "cfg4s": dict(F=96, M=12, n_random=600, n_loops=3),
+    "cfg4m": dict(F=200, M=24, n_random=3000, n_loops=6),
+}
+
+
+def make_graph_large(F, M, n_random, n_loops, seed=0, H=120, W=160, p=3, span=6, period=64,
+                     radius=0.25, noise=0.5, intr=(80.0, 80.0, 80.0, 60.0)) -> Graph:
+    """SURVEY 8d cfg4 recipe: every patch gets an edge to frame i+1, plus
+    ``n_random`` random edges with |j - i| <= span, plus ``n_loops`` loop blocks
+    (all M slots of frame i observed from frame i + k*period, k >= 1).  The
+    trajectory is periodic (a small loop every ``period`` frames, deviation
+    from the reference recipe's straight line) so that loop edges reproject
+    in front of the camera.  Edges are left in a shuffled order (the solver
+    must group them itself, as after DPVO's append/remove bookkeeping)."""
+    g = torch.Generator().manual_seed(seed)
+    f = torch.arange(F, dtype=torch.float64)
+    ang = 2 * math.pi * f / period
+    xi = torch.zeros(F, 6, dtype=torch.float64)
+    xi[:, 0] = radius * torch.sin(ang)
+    xi[:, 2] = radius * (1 - torch.cos(ang))
+    xi[:, 4] = 0.05 * torch.sin(ang)
+    xi += 0.005 * torch.randn(F, 6, generator=g, dtype=torch.float64)
+    xi[0] = 0
+    poses_np = se3_exp(xi.numpy())
+    cxy = torch.stack([torch.rand(F * M, generator=g) * (W - 9) + 4,
+                       torch.rand(F * M, generator=g) * (H - 9) + 4], -1).floor()
+    d = torch.rand(F * M, generator=g) * 0.6 + 0.3
+    off = torch.arange(p, dtype=torch.float32) - p // 2
+    patches = torch.zeros(F * M, 3, p, p)
+    patches[:, 0] = cxy[:, 0].view(-1, 1, 1) + off.view(1, 1, p)
+    patches[:, 1] = cxy[:, 1].view(-1, 1, 1) + off.view(1, p, 1)
+    patches[:, 2] = d.view(-1, 1, 1)
+
+    k_next = torch.arange((F - 1) * M)
+    j_next = k_next // M + 1
+    kr = torch.randint(0, F * M, (n_random,), generator=g)
+    ir = kr // M
+    jr = (ir + torch.randint(-span, span + 1, (n_random,), generator=g)).clamp(0, F - 1)
+    kl, jl = [], []
+    starts = torch.randperm(max(F - period, 1), generator=g)[:n_loops]
+    for i0 in starts.tolist():
+        j0 = i0 + period * (1 + (i0 % 2)) if i0 + 2 * period < F else i0 + period
+        j0 = min(j0, F - 1)
+        kl.append(torch.arange(i0 * M, (i0 + 1) * M))
+        jl.append(torch.full((M,), j0, dtype=torch.long))
+    kk = torch.cat([k_next, kr] + kl)
+    jj = torch.cat([j_next, jr] + jl)
+    perm = torch.randperm(len(kk), generator=g)
+    kk, jj = kk[perm].long(), jj[perm].long()
+    ii = kk // M
+    poses = torch.from_numpy(poses_np).float()
+    intrinsics = torch.tensor(intr).view(1, 4).repeat(F, 1)
+    ctr = reproject_centres(poses.double().numpy(), patches.double().numpy(), intr, ii.numpy(),
+                            jj.numpy(), kk.numpy())
+    target = torch.from_numpy(ctr).float() + noise * torch.randn(len(ii), 2, generator=g)
+    weight = torch.rand(len(ii), 2, generator=g)
+    return Graph(poses, patches, intrinsics, ii, jj, kk, target, weight, F, M)
+
+
 def make_config(name, seed=0, **kw) -> Graph:
+    if name in LARGE_CONFIGS:
+        c = dict(LARGE_CONFIGS[name])
+        c.update(kw)
+        return make_graph_large(seed=seed, **c)
     c = dict(CONFIGS[name])
     c.update(kw)
     return make_graph(seed=seed, **c)

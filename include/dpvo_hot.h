@@ -125,12 +125,13 @@ size_t dpvo_ba_workspace_bytes(int E, int t0, int t1);
 /* Instrumentation / testing: which F-BA implementation dpvo_ba_forward uses.
    0 = auto: one persistent workgroup per lower 6x6 block of S (ba_blocks.hip)
    for E <= 2048 edges and N <= 16 free poses, the multi-kernel path (ba.hip)
-   otherwise; 1 = the single-workgroup kernel (ba_fused.hip, E <= 2048,
-   N <= 12); 2 = always the multi-kernel path; 3 = same as 0.  Process-wide. */
+   for E <= 16384 and N <= 20, the large-graph path (ba_large.hip) beyond;
+   1 = the single-workgroup kernel (ba_fused.hip, E <= 2048, N <= 12);
+   2 = the multi-kernel path; 3 = same as 0; 4 = always the large-graph path.
+   Process-wide; call before sizing the workspace. */
 int dpvo_ba_select_path(int mode);
 
-/* Largest number of free poses (t1 - t0) the single-workgroup Schur solve
-   handles in this build. */
+/* Largest number of free poses (t1 - t0) dpvo_ba_forward handles. */
 int dpvo_ba_max_free_poses(void);
 
 /* F-BA.  Replaces cuda_ba.forward (dpvo/fastba/ba.cpp:32-45 -> cuda_ba,
@@ -177,6 +178,40 @@ int dpvo_ba_phase_marks(const void* workspace, int E, int t0, int t1, int64_t* o
    last Schur launch, [2 x N(N+1)/2] int64 to DEVICE `out`. */
 int dpvo_ba_workgroup_marks(const void* workspace, int E, int t0, int t1, int64_t* out,
                             void* stream);
+
+/* F-BA on large graphs (ba_large.hip): DPVO's global BA (dpvo.py:695-715 ->
+   fastba.BA(..., eff_impl=True), block_e.cu:43-300) and the edge-sharded
+   multi-GPU form.  dpvo_ba_forward dispatches here by itself;
+   the split entry points serve the sharded driver:
+     setup   once per call: patch grouping, block-sparse pattern of S and the
+             band / border analysis.  Rank ownership: a patch belongs to this
+             rank iff own_lo <= kk / PPF < own_hi (its source frame); only
+             owned patches (and their edges) are linearised and summed.
+     build   per iteration: linearise the owned edges and write this rank's
+             part of the packed system [y (6N doubles) | S lower 6x6 blocks
+             (nblk x 36 doubles)] at workspace + dpvo_gba_packed_offset().
+             (all_reduce(SUM) of the first 6N + 36 nblk doubles goes here.)
+     solve_update  damp, solve S dX = y (block cyclic reduction + border
+             Schur complement, fp64), retract poses t0..t1-1 and the inverse
+             depth of every OWNED patch.
+   info copies 8 ints to DEVICE `out`: status (bit 0 factorisation failed ->
+   dX = 0, bit 1 kk clamped, bit 2 a patch touches > 24 free poses, bit 3
+   more than 64 poses couple further back than 16 poses -> dX = 0), unique
+   patches, items, nblk, interior poses, border poses, superblock poses g,
+   superblocks.  N <= dpvo_gba_max_free_poses(), E <= 2^22. */
+size_t dpvo_gba_workspace_bytes(int E, int t0, int t1);
+int dpvo_gba_max_free_poses(void);
+size_t dpvo_gba_packed_offset(int E, int t0, int t1);
+int dpvo_gba_setup(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
+                   int PPF, int t0, int t1, int own_lo, int own_hi, void* workspace,
+                   size_t workspace_bytes, void* stream);
+int dpvo_gba_build(const float* poses, const float* patches, const float* intrinsics,
+                   const float* target, const float* weight, const float* lmbda, const int64_t* ii,
+                   const int64_t* jj, int E, int P, int num_poses, int t0, int t1,
+                   void* workspace, void* stream);
+int dpvo_gba_solve_update(float* poses, float* patches, int E, int P, int t0, int t1,
+                          void* workspace, void* stream);
+int dpvo_gba_info(const void* workspace, int E, int t0, int t1, int* out, void* stream);
 
 /* F-REPROJ.  Replaces cuda_ba.reproject (ba.cpp:47-53 -> cuda_reproject,
    ba_cuda.cu:585-616 + reproject :379-429).  coords [E,2,P,P]. */

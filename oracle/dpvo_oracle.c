@@ -509,9 +509,40 @@ static void edge_linearize(const float* poses, const float* patches, int P, floa
    S_out [(6N)^2] (damped Schur matrix before factorisation), y_out [6N].
    Returns 0, or 1 + column on a failed Cholesky (then dX = 0, as
    dpvo/ba.py:17-21 does; ba_cuda.cu does not check info). */
+/* Edge-sharded form, same arithmetic: only edges whose patch
+   belongs to a source frame kk / PPF in [own_lo, own_hi) are linearised, and
+   only those patches are retracted.  phase 0: full iterations (orc_ba);
+   phase 1: one linearisation -> this rank's UNDAMPED S_io [(6N)^2], y_io [6N];
+   phase 2: one step from the GLOBAL (summed, undamped) S_io / y_io: damp,
+   factorise, dX, dZ of owned patches, retractions. */
+static int ba_core(float* poses, float* patches, const float* intrinsics, const float* target,
+                   const float* weight, float lmbda, const int64_t* ii, const int64_t* jj,
+                   const int64_t* kk, int E, int P, int t0, int t1, int iterations, int PPF,
+                   int own_lo, int own_hi, int phase, double* S_io, double* y_io, double* dX_out,
+                   double* dZ_out, double* S_out, double* y_out);
+
 ORC_API int orc_ba(float* poses, float* patches, const float* intrinsics, const float* target,
                    const float* weight, float lmbda, const int64_t* ii, const int64_t* jj,
                    const int64_t* kk, int E, int P, int t0, int t1, int iterations, double* dX_out,
+                   double* dZ_out, double* S_out, double* y_out) {
+  return ba_core(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P, t0, t1,
+                 iterations, 1, -0x7fffffff, 0x7fffffff, 0, NULL, NULL, dX_out, dZ_out, S_out,
+                 y_out);
+}
+
+ORC_API int orc_ba_shard(float* poses, float* patches, const float* intrinsics,
+                         const float* target, const float* weight, float lmbda, const int64_t* ii,
+                         const int64_t* jj, const int64_t* kk, int E, int P, int t0, int t1,
+                         int PPF, int own_lo, int own_hi, int phase, double* S_io, double* y_io) {
+  if (phase != 1 && phase != 2) return -1;
+  return ba_core(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P, t0, t1, 1,
+                 PPF, own_lo, own_hi, phase, S_io, y_io, NULL, NULL, NULL, NULL);
+}
+
+static int ba_core(float* poses, float* patches, const float* intrinsics, const float* target,
+                   const float* weight, float lmbda, const int64_t* ii, const int64_t* jj,
+                   const int64_t* kk, int E, int P, int t0, int t1, int iterations, int PPF,
+                   int own_lo, int own_hi, int phase, double* S_io, double* y_io, double* dX_out,
                    double* dZ_out, double* S_out, double* y_out) {
   const float fx = intrinsics[0], fy = intrinsics[1], cx = intrinsics[2], cy = intrinsics[3];
   const int N = t1 - t0;
@@ -520,7 +551,9 @@ ORC_API int orc_ba(float* poses, float* patches, const float* intrinsics, const 
   const int M = unique_inverse(kk, E, kx, ku); /* ba_cuda.cu:447-449 */
   const int n6 = 6 * (N > 0 ? N : 0);
   double* Bm = (double*)calloc((size_t)n6 * n6 + 1, sizeof(double));
+  /* E stored transposed, [M][6N]: a patch's nonzero rows are contiguous */
   double* Em = (double*)calloc((size_t)n6 * M + 1, sizeof(double));
+  int* nzr = (int*)malloc(sizeof(int) * (n6 + 1));
   double* Cv = (double*)calloc(M + 1, sizeof(double));
   double* v = (double*)calloc(n6 + 1, sizeof(double));
   double* u = (double*)calloc(M + 1, sizeof(double));
@@ -537,6 +570,7 @@ ORC_API int orc_ba(float* poses, float* patches, const float* intrinsics, const 
     memset(v, 0, sizeof(double) * n6);
     memset(u, 0, sizeof(double) * M);
     for (int n = 0; n < E; n++) {
+      if (kk[n] / PPF < own_lo || kk[n] / PPF >= own_hi) continue; /* another rank's patch */
       float w[2], r[2], Jz[2], Ji[2][6], Jj[2][6];
       edge_linearize(poses, patches, P, fx, fy, cx, cy, target + 2 * n, weight + 2 * n, ii[n],
                      jj[n], kk[n], w, r, Jz, Ji, Jj);
@@ -555,8 +589,8 @@ ORC_API int orc_ba(float* poses, float* patches, const float* intrinsics, const 
             }
           }
         for (int a = 0; a < 6; a++) { /* :352-370 */
-          if (fi) Em[(6 * ix + a) * M + k] -= wr * Jz[row] * Ji[row][a];
-          if (fj) Em[(6 * jx + a) * M + k] += wr * Jz[row] * Jj[row][a];
+          if (fi) Em[k * n6 + 6 * ix + a] -= wr * Jz[row] * Ji[row][a];
+          if (fj) Em[k * n6 + 6 * jx + a] += wr * Jz[row] * Jj[row][a];
           if (fi) v[6 * ix + a] -= wr * r[row] * Ji[row][a];
           if (fj) v[6 * jx + a] += wr * r[row] * Jj[row][a];
         }
@@ -569,15 +603,32 @@ ORC_API int orc_ba(float* poses, float* patches, const float* intrinsics, const 
     if (N <= 0) { /* structure only, :521-531 */
       for (int k = 0; k < M; k++) dZ[k] = Q[k] * u[k];
     } else {
-      for (int a = 0; a < n6; a++) { /* S = B - E Q E^T ; y = v - E Q u (:554-558) */
-        double ya = v[a];
-        for (int k = 0; k < M; k++) ya -= Em[a * M + k] * Q[k] * u[k];
-        y[a] = ya;
-        for (int b = 0; b < n6; b++) {
-          double s = Bm[a * n6 + b];
-          for (int k = 0; k < M; k++) s -= Em[a * M + k] * Q[k] * Em[b * M + k];
-          S[a * n6 + b] = s;
+      /* S = B - E Q E^T ; y = v - E Q u (:554-558).  Per entry the patches are
+         summed in ascending k; zero terms of E are skipped (exact no-ops). */
+      if (phase == 2) {
+        memcpy(Bm, S_io, sizeof(double) * n6 * n6);
+        memcpy(v, y_io, sizeof(double) * n6);
+      }
+      memcpy(S, Bm, sizeof(double) * n6 * n6);
+      memcpy(y, v, sizeof(double) * n6);
+      for (int k = 0; k < M && phase != 2; k++) {
+        const double* ek = Em + (size_t)k * n6;
+        int nz = 0;
+        for (int a = 0; a < n6; a++)
+          if (ek[a] != 0.0) nzr[nz++] = a;
+        for (int x = 0; x < nz; x++) {
+          const int a = nzr[x];
+          y[a] -= ek[a] * Q[k] * u[k];
+          for (int z = 0; z < nz; z++) {
+            const int b = nzr[z];
+            S[(size_t)a * n6 + b] -= ek[a] * Q[k] * ek[b];
+          }
         }
+      }
+      if (phase == 1) {
+        memcpy(S_io, S, sizeof(double) * n6 * n6);
+        memcpy(y_io, y, sizeof(double) * n6);
+        break;
       }
       for (int a = 0; a < n6; a++) S[a * n6 + a] += 1e-4 * S[a * n6 + a] + 1.0; /* :560 */
       if (S_out) memcpy(S_out, S, sizeof(double) * n6 * n6);
@@ -591,7 +642,7 @@ ORC_API int orc_ba(float* poses, float* patches, const float* intrinsics, const 
       }
       for (int k = 0; k < M; k++) { /* dZ = Q (u - E^T dX) (:563) */
         double s = u[k];
-        for (int a = 0; a < n6; a++) s -= Em[a * M + k] * y[a];
+        for (int a = 0; a < n6; a++) s -= Em[(size_t)k * n6 + a] * y[a];
         dZ[k] = Q[k] * s;
       }
       for (int i = 0; i < N; i++) { /* pose_retr_kernel :178-206 */
@@ -604,7 +655,9 @@ ORC_API int orc_ba(float* poses, float* patches, const float* intrinsics, const 
       }
       if (dX_out) memcpy(dX_out, y, sizeof(double) * n6);
     }
+    if (phase == 1) break;
     for (int k = 0; k < M; k++) { /* patch_retr_kernel :209-229 */
+      if (kx[k] / PPF < own_lo || kx[k] / PPF >= own_hi) continue;
       float* pk = patches + (size_t)kx[k] * 3 * P * P;
       float d = pk[2 * P * P + 0];
       d = d + (float)dZ[k];
@@ -614,7 +667,7 @@ ORC_API int orc_ba(float* poses, float* patches, const float* intrinsics, const 
     }
     if (dZ_out) memcpy(dZ_out, dZ, sizeof(double) * M);
   }
-  free(kx); free(ku); free(Bm); free(Em); free(Cv); free(v); free(u); free(Q); free(S); free(y);
+  free(kx); free(ku); free(Bm); free(Em); free(nzr); free(Cv); free(v); free(u); free(Q); free(S); free(y);
   free(dZ);
   return status;
 }

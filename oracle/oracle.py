@@ -211,3 +211,34 @@ def lie_bwd(group, op, grad, x, y=None):
     if op in ("exp", "log", "inv"):
         return (o0,)
     return (o0, o1)
+
+
+def ba_shard(phase, poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, PPF,
+             own_lo, own_hi, S=None, y=None):
+    """Edge-sharded BA step of the C oracle (ba_core in dpvo_oracle.c), test
+    infrastructure for the multi-rank driver.  phase 1: returns this rank's
+    undamped (S [6N, 6N], y [6N]) over patches with own_lo <= kk // PPF <
+    own_hi.  phase 2: applies one step from the GLOBAL (S, y) in place on the
+    given poses / patches (numpy float32 arrays, modified) and returns them."""
+    P = np.shape(patches)[-1]
+    N = max(t1 - t0, 0)
+    ii, jj, kk = _i64(ii), _i64(jj), _i64(kk)
+    E = ii.shape[0]
+    if phase == 1:
+        poses, patches = _f32(poses).reshape(-1, 7), _f32(patches).reshape(-1, 3, P, P)
+        S = np.zeros(36 * N * N + 1, np.float64)
+        y = np.zeros(6 * N + 1, np.float64)
+    else:
+        assert poses.dtype == np.float32 and patches.dtype == np.float32
+        assert poses.flags.c_contiguous and patches.flags.c_contiguous
+        S = np.concatenate([_f64(S).reshape(-1), [0.0]])
+        y = np.concatenate([_f64(y).reshape(-1), [0.0]])
+    rc = lib().orc_ba_shard(_p(poses), _p(patches), _p(_f32(intrinsics).reshape(-1, 4)),
+                            _p(_f32(target).reshape(-1, 2)), _p(_f32(weight).reshape(-1, 2)),
+                            ctypes.c_float(float(np.asarray(lmbda).reshape(-1)[0])), _p(ii), _p(jj),
+                            _p(kk), E, P, int(t0), int(t1), int(PPF), int(own_lo), int(own_hi),
+                            int(phase), _p(S), _p(y))
+    _check(rc, "ba_shard")
+    if phase == 1:
+        return S[:36 * N * N].reshape(6 * N, 6 * N), y[:6 * N]
+    return poses, patches

@@ -12,7 +12,7 @@ STEPS="${STEPS:-tests smoke bench prof}"
 for s in $STEPS; do
   case $s in
     ba) timeout -k 10 240 python -m pytest tests/test_ba_gpu.py -q -rf > $OUT/ba_gpu.log 2>&1; rc=$?;;
-    tests) timeout -k 10 900 python -m pytest tests -m gpu -q -rf > $OUT/pytest_gpu.log 2>&1; rc=$?;;
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?;;
     bench) timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; rc=$?;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 50 --warmup 10 --no-cpu-baseline > $OUT/prof.log 2>&1; rc=$?;;

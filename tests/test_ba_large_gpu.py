@@ -1,0 +1,168 @@
+"""GPU parity of the large-graph F-BA (ba_large.hip: DPVO's global BA,
+fastba.BA(..., eff_impl=True) on >20 free poses, BASELINE cfg4) against the
+oracle (ba_cuda.cu / block_e.cu semantics, dense S + Cholesky), plus the
+edge-sharded split emulated on one GPU.
+
+Graphs: synthetic.make_graph_large (cfg4 recipe: next-frame edges, random
+|j - i| <= 6 edges, loop blocks -> border poses), edges in shuffled order.
+Tolerances as tests/test_ba_gpu.py: poses 2e-5 abs, inverse depths 1e-4 rel
++ 1e-5; dX relative 2-norm <= 1e-4 (north_star)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from dpvo_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cb(gpu):
+    import dpvo_amd
+
+    return dpvo_amd.load_extension("cuda_ba")
+
+
+def _oracle(G, t0, t1, iters):
+    return oracle.ba(G.poses.numpy(), G.patches.numpy(), G.intrinsics.numpy(), G.target.numpy(),
+                     G.weight.numpy(), 1e-4, G.ii.numpy(), G.jj.numpy(), G.kk.numpy(), t0, t1,
+                     iters)
+
+
+def _gpu(cb, G, gpu, t0, t1, iters, eff=True):
+    D = G.to(gpu)
+    poses, patches = D.poses.clone(), D.patches.clone()
+    cb.forward(poses, patches, D.intrinsics, D.target, D.weight, torch.tensor([1e-4], device=gpu),
+               D.ii, D.jj, D.kk, G.M, t0, t1, iters, eff)
+    torch.cuda.synchronize()
+    return poses.cpu().numpy(), patches.cpu().numpy()
+
+
+def _check(P, K, Pr, Kr):
+    np.testing.assert_allclose(P, Pr, rtol=0, atol=2e-5)
+    np.testing.assert_allclose(K[:, 2], Kr[:, 2], rtol=1e-4, atol=1e-5)
+    np.testing.assert_array_equal(K[:, :2], Kr[:, :2])
+
+
+def _info(cb, G, gpu, t0, t1, own=(-(2**31) + 1, 2**31 - 1)):
+    D = G.to(gpu)
+    ws = cb.gba_setup(D.ii, D.jj, D.kk, D.patches.shape[0], G.M, t0, t1, *own)
+    return ws, D, cb.gba_info(ws, G.E, t0, t1).cpu().tolist()
+
+
+@pytest.mark.parametrize("cfg,iters", [("cfg4s", 1), ("cfg4s", 2), ("cfg4m", 2)])
+def test_large_matches_oracle(cb, gpu, cfg, iters):
+    G = synthetic.make_config(cfg, seed=1)
+    P, K = _gpu(cb, G, gpu, 1, G.F, iters)
+    Pr, Kr = _oracle(G, 1, G.F, iters)
+    _check(P, K, Pr, Kr)
+
+
+def test_large_structure_has_border_and_band(cb, gpu):
+    G = synthetic.make_config("cfg4s", seed=1)
+    _, _, info = _info(cb, G, gpu, 1, G.F)
+    status, nuniq, nitems, nblk, nI, nB, g, nsb = info
+    assert status == 0
+    assert nuniq == len(np.unique(G.kk.numpy()))
+    assert nI + nB == G.F - 1 and 1 <= nB <= 3  # loop targets go to the border
+    assert 1 <= g <= 16 and nsb == -(-nI // g)
+
+
+def test_forced_large_path_on_window_graph(cb, gpu):
+    # the large-graph path on a DPVO window (cfg2) agrees with the oracle too
+    G = synthetic.make_config("cfg2", seed=2)
+    cb.select_path(4)
+    try:
+        P, K = _gpu(cb, G, gpu, 1, G.F, 2, eff=False)
+    finally:
+        cb.select_path(0)
+    Pr, Kr = _oracle(G, 1, G.F, 2)
+    _check(P, K, Pr, Kr)
+
+
+def test_large_fixed_prefix_and_structure_only(cb, gpu):
+    G = synthetic.make_config("cfg4s", seed=4)
+    P, K = _gpu(cb, G, gpu, 30, G.F, 1)  # poses < 30 fixed
+    Pr, Kr = _oracle(G, 30, G.F, 1)
+    _check(P, K, Pr, Kr)
+    np.testing.assert_array_equal(P[:30], G.poses.numpy()[:30])
+    P, K = _gpu(cb, G, gpu, 5, 5, 2)  # structure only (t0 == t1)
+    Pr, Kr = _oracle(G, 5, 5, 2)
+    _check(P, K, Pr, Kr)
+
+
+def test_large_is_deterministic(cb, gpu):
+    G = synthetic.make_config("cfg4m", seed=5)
+    a = _gpu(cb, G, gpu, 1, G.F, 2)
+    b = _gpu(cb, G, gpu, 1, G.F, 2)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+
+
+def test_sharded_split_emulated_on_one_gpu(cb, gpu):
+    """Two 'ranks' (frame ranges) on one GPU: the sum of their packed (y, S)
+    equals the unsharded system; solving it reproduces the unsharded BA."""
+    G = synthetic.make_config("cfg4s", seed=6)
+    t0, t1 = 1, G.F
+    lm = torch.tensor([1e-4], device=gpu)
+    cut = G.F // 2
+    ranges = [(-(2**31) + 1, cut), (cut, 2**31 - 1)]
+    full_ws, D, info = _info(cb, G, gpu, t0, t1)
+    nblk = info[3]
+    poses_f, patches_f = D.poses.clone(), D.patches.clone()
+    cb.gba_build(full_ws, poses_f, patches_f, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj,
+                 t0, t1)
+    full = cb.gba_packed(full_ws, G.E, t0, t1, nblk).clone()
+    parts, wss = [], []
+    for r in ranges:
+        ws, _, inf = _info(cb, G, gpu, t0, t1, r)
+        assert inf[3] == nblk  # same global pattern on every rank
+        cb.gba_build(ws, D.poses, D.patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj,
+                     t0, t1)
+        parts.append(cb.gba_packed(ws, G.E, t0, t1, nblk))
+        wss.append(ws)
+    total = parts[0] + parts[1]
+    torch.testing.assert_close(total, full, rtol=1e-10, atol=1e-9)
+    outs = []
+    for ws, p in zip(wss, parts):
+        p.copy_(total)  # the all_reduce
+        poses, patches = D.poses.clone(), D.patches.clone()
+        cb.gba_solve_update(ws, poses, patches, G.E, t0, t1)
+        outs.append((poses, patches))
+    cb.gba_solve_update(full_ws, poses_f, patches_f, G.E, t0, t1)
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=0, atol=0)  # identical solve
+    torch.testing.assert_close(outs[0][0], poses_f, rtol=0, atol=1e-6)
+    own0 = (torch.arange(D.patches.shape[0], device=gpu) // G.M) < cut
+    depth = torch.where(own0[:, None, None], outs[0][1][:, 2], outs[1][1][:, 2])
+    torch.testing.assert_close(depth, patches_f[:, 2], rtol=1e-6, atol=1e-7)
+
+
+def test_cfg4_full_size_runs_and_agrees_with_sharded(cb, gpu):
+    """BASELINE cfg4 (1024 x 96, ~131k edges, N = 1023): status clean, the
+    expected border, finite steps, deterministic, and 4 emulated ranks give
+    the same packed system as 1."""
+    G = synthetic.make_config("cfg4", seed=0)
+    t0, t1 = 1, G.F
+    ws, D, info = _info(cb, G, gpu, t0, t1)
+    status, nuniq, nitems, nblk, nI, nB, g, nsb = info
+    assert status == 0 and nuniq == G.F * G.M and nB <= 10 and g <= 16
+    P1, K1 = _gpu(cb, G, gpu, t0, t1, 2)
+    P2, K2 = _gpu(cb, G, gpu, t0, t1, 2)
+    np.testing.assert_array_equal(P1, P2)
+    np.testing.assert_array_equal(K1, K2)
+    assert np.isfinite(P1).all() and np.isfinite(K1).all()
+    dpose = np.abs(P1 - G.poses.numpy()).max()
+    assert 0 < dpose < 0.5
+    lm = torch.tensor([1e-4], device=gpu)
+    cb.gba_build(ws, D.poses, D.patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj, t0, t1)
+    full = cb.gba_packed(ws, G.E, t0, t1, nblk).clone()
+    from dpvo_amd.fastba.sharded import frame_partition
+
+    tot = torch.zeros_like(full)
+    for r in frame_partition(D.kk, G.M, 4):
+        w2 = cb.gba_setup(D.ii, D.jj, D.kk, D.patches.shape[0], G.M, t0, t1, *r)
+        cb.gba_build(w2, D.poses, D.patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj,
+                     t0, t1)
+        tot += cb.gba_packed(w2, G.E, t0, t1, nblk)
+    torch.testing.assert_close(tot, full, rtol=1e-9, atol=1e-8)
