@@ -119,10 +119,13 @@ def main():
     def step(i=0, ev=None):
         slot = i % args.mem  # frame insertion (dpvo.py:__call__ -> ring buffer)
         altcorr.insert_frame(pyr_nchw[0][0, slot], pyr, slot, levels)
-        coords = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk)
+        # reprojection + the XCD-aware edge order (edges grouped by target
+        # frame) in one launch; A-CORR processes each group on one XCD
+        coords, order = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk,
+                                         mem=args.mem)
         if ev is not None:
             ev[0].record()
-        corr = altcorr.corr_levels(gbuf, pyr, coords, kk1, jj1, 3, scales)
+        corr = altcorr.corr_levels(gbuf, pyr, coords, kk1, jj1, 3, scales, order=order)
         if ev is not None:
             ev[1].record()
         fastba.BA(poses, patches, D.intrinsics, D.target, D.weight, lmbda, D.ii, D.jj, D.kk, 1,

@@ -113,14 +113,16 @@ def insert_frame(fmap, pyramid, slot, scales=(1, 4)):
                                      [int(s) for s in scales])
 
 
-def corr_levels(fmap1, pyramid, coords, ii, jj, radius=3, scales=(1, 4)):
+def corr_levels(fmap1, pyramid, coords, ii, jj, radius=3, scales=(1, 4), order=None):
     """DPVO.corr (dpvo/dpvo.py:456-465) in ONE launch: correlation of every
     pyramid level (coords divided by each level's scale) stacked on the last
     axis and flattened to [B, M, (2R+1)^2 * p^2 * L] float32.  Inference only.
 
     Levels stored channels-last (``synthetic.channels_last`` / ``to_channels_last``)
-    take the matrix-core path (corr_nhwc.hip); NCHW levels the VALU path."""
+    take the matrix-core path (corr_nhwc.hip); NCHW levels the VALU path.
+    ``order`` (int32 [E], from ``fastba.reproject(..., mem=N2)``): process
+    edges grouped by target frame, one group range per XCD (same results)."""
     require_gpu(fmap1)
     out = cuda_corr.forward_levels(fmap1, list(pyramid), coords, ii, jj, radius,
-                                   [float(s) for s in scales])
+                                   [float(s) for s in scales], order)
     return out.view(out.shape[0], out.shape[1], -1)

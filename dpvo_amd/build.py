@@ -37,6 +37,11 @@ EXTENSIONS = {
     "lietorch_backends": "ext_lietorch.cpp",
 }
 HEADERS = ["common.hpp", "ext_common.hpp", "ba_device.hpp"]
+# per-source device flags.  The BA window kernel is a chain of short dependent
+# steps run by few waves: clang's SLP vectoriser packs its scalar fp32 math into
+# v_pk_fma_f32 and pays for it with register-pair v_mov shuffles (3x the
+# instructions of the 6x6 pivot factorisation), so it is off there.
+SOURCE_FLAGS = {"ba_blocks.hip": ["-fno-slp-vectorize"]}
 
 
 def _git_rev():
@@ -87,7 +92,8 @@ def build(force=False, verbose=False):
         if force or _stale(obj, [src] + hdr + [__file__]):
             cmd = [hipcc, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c",
                    "-fvisibility=hidden", "-mcode-object-version=5", "-Wno-unused-result",
-                   f"-I{INCLUDE}", f'-DDPVO_GIT_REV="{_git_rev()}"', src, "-o", obj]
+                   f"-I{INCLUDE}", f'-DDPVO_GIT_REV="{_git_rev()}"',
+                   *SOURCE_FLAGS.get(os.path.basename(src), []), src, "-o", obj]
             _run(cmd, verbose)
     if force or _stale(lib, objs):
         cmd = [hipcc, f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-o", lib]

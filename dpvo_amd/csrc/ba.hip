@@ -430,7 +430,13 @@ __global__ void reproject_kernel(const float* __restrict__ poses, const float* _
                                  const float* __restrict__ intrinsics,
                                  const int64_t* __restrict__ ii, const int64_t* __restrict__ jj,
                                  const int64_t* __restrict__ kk, int E, int P, int num_poses,
-                                 int num_patches, float* __restrict__ coords) {
+                                 int num_patches, float* __restrict__ coords,
+                                 int* __restrict__ order, int N2) {
+  if (order && blockIdx.x == gridDim.x - 1) {  // extra workgroup: A-CORR edge order
+    __shared__ int bins[kOrderBins + 1];
+    edge_order_block(jj, E, N2, order, bins);
+    return;
+  }
   const int PP = P * P;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= E * PP) return;
@@ -1157,6 +1163,15 @@ DPVO_EXPORT int dpvo_ba_select_path(int mode) {
   return DPVO_OK;
 }
 
+namespace dpvo {
+void ba_blocks_set_refine(int on);
+}
+DPVO_EXPORT int dpvo_ba_set_refine(int on) {
+  if (on < 0 || on > 2) return DPVO_ERR_INVALID;
+  dpvo::ba_blocks_set_refine(on);
+  return DPVO_OK;
+}
+
 DPVO_EXPORT int dpvo_ba_max_free_poses(void) { return dpvo_gba_max_free_poses(); }
 
 DPVO_EXPORT int dpvo_ba_setup(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E,
@@ -1316,7 +1331,22 @@ DPVO_EXPORT int dpvo_reproject(const float* poses, const float* patches, const f
   const int total = E * P * P;
   hipLaunchKernelGGL(reproject_kernel, dim3((total + 255) / 256), dim3(256), 0,
                      as_stream(stream), poses, patches, intrinsics, ii, jj, kk, E, P, num_poses,
-                     num_patches, coords);
+                     num_patches, coords, (int*)nullptr, 0);
+  return launch_status();
+}
+
+DPVO_EXPORT int dpvo_reproject_ordered(const float* poses, const float* patches,
+                                       const float* intrinsics, const int64_t* ii,
+                                       const int64_t* jj, const int64_t* kk, int E, int P,
+                                       int num_poses, int num_patches, int N2, float* coords,
+                                       int32_t* order, void* stream) {
+  if (E <= 0) return DPVO_OK;
+  if (P <= 0 || num_poses <= 0 || num_patches <= 0 || !order) return DPVO_ERR_INVALID;
+  const int total = E * P * P;
+  // one more workgroup than the reprojection needs: it writes the edge order
+  hipLaunchKernelGGL(reproject_kernel, dim3((total + 255) / 256 + 1), dim3(256), 0,
+                     as_stream(stream), poses, patches, intrinsics, ii, jj, kk, E, P, num_poses,
+                     num_patches, coords, (int*)order, N2);
   return launch_status();
 }
 

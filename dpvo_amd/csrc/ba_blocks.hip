@@ -78,6 +78,7 @@ struct BArgs {
   int* kxw;        // [NB][E]     patch id of each relevant patch, -1 if not owned
   float* dbw;      // [NB][E]     first-iteration retraction base [2][0][0]
   int* meta;       // [8] [0] nuniq, [1] status
+  int refine;      // solve mode: 0 fp32 Cholesky, 1 + fp64 refinement, 2 fp64 block LDL^T
   int64_t* marks;  // [64] wall-clock stamps of workgroup 0 (may be null)
 };
 
@@ -120,7 +121,7 @@ __device__ __forceinline__ void bstamp(const BArgs& A, int slot) {
 }
 
 // ---------------------------------------------------------------------------
-// block LDL^T solve of the damped S (workgroup 0).  S: lower blocks in LDS.
+// fp64 block LDL^T solve of the damped S (workgroup 0; solve mode 2).  S: lower blocks in LDS.
 // ---------------------------------------------------------------------------
 struct Solver {
   double* S;    // [NB][36]
@@ -758,8 +759,9 @@ __global__ void __launch_bounds__(kBT) ba_blocks_kernel(BArgs A) {
     // scratch = [reduction table | solver (workgroup 0)] then, if they fit,
     // the per-edge entries and per-patch (Q, u) of the iteration in flight
     const size_t red_bytes = sizeof(double) * (kV * kRedCols + kV * 8);
-    const size_t NN = (size_t)(N > 0 ? N : 1), NBp = (size_t)(NB > 0 ? NB : 1);
-    const size_t solve_bytes = sizeof(double) * (36 * NBp + 6 * NN + 36 * NN + 12 * NN + 36 * NN);
+    const size_t NN = (size_t)(N > 0 ? N : 1);
+    const size_t s32 = solver32_bytes((int)NN), s64 = sizeof(double) * (36 * NN * (NN + 1) / 2 + 90 * NN);
+    const size_t solve_bytes = s32 > s64 ? s32 : s64;
     size_t o2 = al16(o + (red_bytes > solve_bytes ? red_bytes : solve_bytes));
     const size_t pe_bytes = al16(sizeof(double) * 14 * (size_t)(nrp > 0 ? nrp : 1));
     const size_t pq_bytes = al16(sizeof(double2) * (size_t)(nrel > 0 ? nrel : 1));
@@ -920,13 +922,17 @@ __global__ void __launch_bounds__(kBT) ba_blocks_kernel(BArgs A) {
     // ---- workgroup 0: gather S, solve, publish dX ----
     if (g == 0) {
       const int NN = N > 0 ? N : 1;
-      Solver sv;
-      sv.S = (double*)L.scratch;
-      sv.y = sv.S + 36 * (NB > 0 ? NB : 1);
-      sv.piv = sv.y + 6 * NN;
-      sv.wv = sv.piv + 36 * NN;
-      sv.tt = sv.wv + 6 * NN;
-      sv.PV = sv.tt + 6 * NN;
+      Solver32 sv;
+      double* Sd = (double*)L.scratch;  // gathered + damped S, then y
+      double* yd = Sd + 36 * (NB > 0 ? NB : 1);
+      sv.S = Sd;
+      sv.y = yd;
+      sv.x = yd + 6 * NN;
+      sv.part = sv.x + 6 * NN;
+      sv.A = (float*)(sv.part + 24 * NN);
+      sv.Li = sv.A + 36 * (NB > 0 ? NB : 1);
+      sv.w = sv.Li + 36 * NN;
+      sv.Nf = sv.w + 6 * NN;
       double* dXo = A.dXg + (size_t)(it & 1) * 6 * N;
       if (NB > 0) {
         for (int w = tid; w < 2 * NB; w += T)  // one lane per arrival flag
@@ -945,19 +951,30 @@ __global__ void __launch_bounds__(kBT) ba_blocks_kernel(BArgs A) {
             }
 #pragma unroll
             for (int r = 0; r < 8; r++)
-              if (k0 + r * T < tot) sv.S[k0 + r * T] = v0[r] + v1[r];
+              if (k0 + r * T < tot) Sd[k0 + r * T] = v0[r] + v1[r];
           }
-          for (int k = tid; k < 6 * N; k += T) sv.y[k] = A.yg[k] + A.yg[6 * N + k];
+          for (int k = tid; k < 6 * N; k += T) yd[k] = A.yg[k] + A.yg[6 * N + k];
         }
         __syncthreads();
         for (int k = tid; k < 6 * N; k += T) {  // S += I (1e-4 S + 1) (ba_cuda.cu:560)
-          double* d = sv.S + 36 * lblk(k / 6, k / 6) + 7 * (k % 6);
+          double* d = Sd + 36 * lblk(k / 6, k / 6) + 7 * (k % 6);
           *d += 1e-4 * *d + 1.0;
         }
         if (tid == 0) ctl[kCFail] = 0;
         __syncthreads();
         bstamp(A, mb + 3);
-        block_ldl_solve(sv, N, L.dX, &ctl[kCFail], A.marks ? A.marks + mb : nullptr);
+        if (A.refine == 2) {
+          Solver sd;  // fp64 LDL^T in the same scratch (S, y in place)
+          sd.S = Sd;
+          sd.y = yd;
+          sd.piv = yd + 6 * NN;
+          sd.wv = sd.piv + 36 * NN;
+          sd.tt = sd.wv + 6 * NN;
+          sd.PV = sd.tt + 6 * NN;
+          block_ldl_solve(sd, N, L.dX, &ctl[kCFail], A.marks ? A.marks + mb : nullptr);
+        } else {
+          chol32_solve(sv, N, L.dX, &ctl[kCFail], A.refine == 1, A.marks ? A.marks + mb : nullptr);
+        }
         bstamp(A, mb + 5);
         const bool fail = ctl[kCFail] != 0 || ctl[kCTimeout] != 0;
         if (tid < 64)  // wave 0 writes: its own release fence below covers the stores
@@ -1024,6 +1041,9 @@ std::mutex g_flag_mu;
 std::map<int, long long*> g_flags;  // per device (streams share it: see below)
 }  // namespace
 
+static int g_blocks_refine = 2;  // fp64 block LDL^T (dpvo_ba_set_refine: fastest measured)
+void ba_blocks_set_refine(int mode) { g_blocks_refine = mode; }
+
 static long long* flag_slot(hipStream_t st) {
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -1089,6 +1109,7 @@ int ba_blocks_launch(float* poses, float* patches, const float* intrinsics, cons
   a.dbw = (float*)s;
   a.meta = meta;
   a.marks = marks;
+  a.refine = g_blocks_refine;
   hipLaunchKernelGGL(ba_blocks_kernel, dim3(G), dim3(kBT), kBLds, st, a);
   return launch_status();
 }

@@ -64,6 +64,46 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// --- edge order by target frame (XCD-aware A-CORR scheduling) -------------------
+// One workgroup: order[p] = the edge at position p when edges are grouped by
+// their target frame jj (counting sort; the order inside a group is whatever
+// the LDS atomics give -- A-CORR results do not depend on it, every edge is
+// computed independently).  bins: >= kOrderBins + 1 ints of LDS.  Keys outside
+// [0, min(N2, kOrderBins)) share the last bin.
+constexpr int kOrderBins = 1024;
+__device__ inline void edge_order_block(const int64_t* __restrict__ jj, int E, int N2,
+                                        int* __restrict__ order, int* bins) {
+  const int tid = threadIdx.x, T = blockDim.x;
+  const int nb = min(max(N2, 1), kOrderBins);
+  for (int b = tid; b <= nb; b += T) bins[b] = 0;
+  __syncthreads();
+  for (int e = tid; e < E; e += T) {
+    const int64_t v = jj[e];
+    atomicAdd(&bins[(v >= 0 && v < nb) ? (int)v : nb - 1], 1);
+  }
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of nb <= 1024 bins by one wave
+    int carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+      const int b = b0 + tid;
+      const int c = (b < nb) ? bins[b] : 0;
+      int x = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (tid >= o) x += y;
+      }
+      if (b < nb) bins[b] = carry + x - c;
+      carry += __shfl(x, 63, 64);
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < E; e += T) {
+    const int64_t v = jj[e];
+    order[atomicAdd(&bins[(v >= 0 && v < nb) ? (int)v : nb - 1], 1)] = e;
+  }
+}
+
 // --- fp32 SE3 primitives of ba_cuda.cu:36-174 (restated, device) ---------------
 // No FMA contraction here: the per-edge arithmetic then rounds exactly like the
 // C oracle (x86, no FMA), which keeps the parity tests tight.

@@ -19,12 +19,20 @@
 // stored once per edge as contiguous [.., L] float4 rows.
 #include "common.hpp"
 
+// diagnostic builds (scripts/micro/corr_bench.hip) define CORR_STAMP(slot) to
+// record per-wave shader-clock stamps; the library compiles it away
+#ifndef CORR_STAMP
+#define CORR_STAMP(slot)
+#define CORR_STAMP_RT(slot)
+#define CORR_STAMP_ID(slot)
+#endif
+
 namespace dpvo {
 
 constexpr int kNhwcWaves = 4;   // edges per workgroup
 constexpr int kNhwcC = 128;     // channels (DPVO gmap / fmap width)
 constexpr int kMaxTiles = 10;   // box up to 160 pixels through the matrix path
-constexpr int kBoxStride = 16 * kMaxTiles;
+constexpr int kBoxStride = 16 * kMaxTiles + 4;  // +4: the 4 row groups of a G tile store hit distinct LDS banks
 constexpr int kMaxL = 4;        // levels per launch
 constexpr int kOutPerLane = 8;  // (2R+1)^2 * p*p <= 512 outputs per level
 constexpr int kNpMax = 16;      // p*p <= 16 (one MFMA row tile)
@@ -38,165 +46,311 @@ struct NhwcLevels {
 struct NhwcGeom {
   int x0[kNpMax], y0[kNpMax];
   float dx[kNpMax], dy[kNpMax];
+  int xlo, ylo, bw, bh, ntile, pad[3];  // the level's (wave-uniform) box
 };
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__global__ void __launch_bounds__(kNhwcWaves* kWave)
+// One wave per edge, every level (the gmap patch and the coordinates are
+// loaded once per edge).  The kernel is latency-bound: at DPVO sizes there
+// are only 8 edges per CU, so the bytes each wave keeps in flight decide the
+// bandwidth.  Design:
+//  * the gmap patch arrives with 16-B coalesced loads, staged through LDS;
+//  * the geometry of every level is computed up front (power-of-two level
+//    scales are applied as exact reciprocal multiplies);
+//  * the box tiles of all levels form ONE flattened sequence with two more
+//    tiles in flight (a 3-deep register ring; 4 deep would need > 256 VGPRs
+//    and halve the occupancy) while the current one multiplies; the loop body
+//    is not unrolled (the bilinear is inlined once): kernel code stays small;
+//  * a level's bilinear + permute runs as soon as its last tile is in LDS,
+//    from per-lane output codes computed once (no integer division per level).
+
+__global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 waves) per CU: every edge resident at once
     corr_nhwc_kernel(const float* __restrict__ fmap1, NhwcLevels lv, int L,
                      const float* __restrict__ coords, const int64_t* __restrict__ ii,
                      const int64_t* __restrict__ jj, int B, int M, int np, int N1, int N2, int R,
-                     float* __restrict__ out) {
+                     const int* __restrict__ order, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int wid = wave_uniform(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
-  float* G = smem + wid * (kNpMax * kBoxStride);
-  NhwcGeom* geo = reinterpret_cast<NhwcGeom*>(smem + kNhwcWaves * kNpMax * kBoxStride) + wid;
-  const int unit = blockIdx.x * kNhwcWaves + wid;
-  if (unit >= B * M) return;  // waves are independent: no block barrier below
-  const int b = unit / M, m = unit % M;
+  float* G = smem + wid * (np * kBoxStride);
+  NhwcGeom* geo = reinterpret_cast<NhwcGeom*>(smem + kNhwcWaves * np * kBoxStride) + wid * kMaxL;
+  int edge;
+  if (order) {
+    // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so
+    // workgroup w runs on XCD w % 8.  XCD x takes the x-th eighth of the edges
+    // grouped by target frame (order[], B == 1): a frame's coarse levels then
+    // stay in that XCD's 4 MB L2 instead of being fetched by every XCD.
+    const int nwg = (M + kNhwcWaves - 1) / kNhwcWaves, per = (nwg + 7) / 8;
+    const int chunk = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    const int p = chunk * kNhwcWaves + wid;
+    if (chunk >= nwg || p >= M) return;
+    edge = wave_uniform(order[p]);
+  } else {
+    edge = blockIdx.x * kNhwcWaves + wid;
+    if (edge >= B * M) return;  // waves are independent: no block barrier below
+  }
+  const int b = edge / M, m = edge % M;
+  CORR_STAMP(0);
+  CORR_STAMP_RT(12);
+  CORR_STAMP_ID(14);
   const int ix = wave_uniform((int)ii[m]), jx = wave_uniform((int)jj[m]);
   const bool idx_ok = ix >= 0 && ix < N1 && jx >= 0 && jx < N2;
   const int C = kNhwcC, D = 2 * R + 2, Dp = D - 1, nout = Dp * Dp * np;
+  const float cv = (lane < 2 * np) ? coords[((size_t)b * M + m) * 2 * np + lane] : 0.f;
 
-  // ---- A fragments: lane (i = lane & 15, q = lane >> 4) holds f1[c][i] for
+  // ---- gmap patch [C][np] -> LDS (in G, free until the first tile) -> A
+  // fragments: lane (i = lane & 15, q = lane >> 4) holds f1[c][i] for
   // c = 16h + 4q + s at K step 4h + s (the same channel order as the B loads)
   const int ai = lane & 15, aq = lane >> 4;
   float Af[kNhwcC / 4];
   {
     const float* f1 = fmap1 + ((size_t)b * N1 + (idx_ok ? ix : 0)) * C * np;
+    const int n4 = (C * np) >> 2;  // C * np is a multiple of 4 (C = 128)
+    float4 st[(kNhwcC * kNpMax / 4 + kWave - 1) / kWave];
+#pragma unroll
+    for (int r = 0; r < (kNhwcC * kNpMax / 4 + kWave - 1) / kWave; r++) {
+      const int v = lane + kWave * r;
+      st[r] = (v < n4) ? reinterpret_cast<const float4*>(f1)[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int r = 0; r < (kNhwcC * kNpMax / 4 + kWave - 1) / kWave; r++) {
+      const int v = lane + kWave * r;
+      if (v < n4) reinterpret_cast<float4*>(G)[v] = st[r];
+    }
+    wave_lds_sync();
     const bool arow = idx_ok && ai < np;
 #pragma unroll
     for (int h = 0; h < kNhwcC / 16; h++)
 #pragma unroll
       for (int s = 0; s < 4; s++)
-        Af[4 * h + s] = arow ? f1[(size_t)(16 * h + 4 * aq + s) * np + ai] : 0.0f;
+        Af[4 * h + s] = arow ? G[(16 * h + 4 * aq + s) * np + ai] : 0.0f;
   }
 
+  // ---- geometry of every level up front, lane-parallel: lane (l = lane >> 4,
+  // k = lane & 15) takes patch pixel k at level l (floor / frac), 16-lane
+  // min / max reductions give each level's box (kept in LDS: levels are
+  // indexed dynamically below)
+  int cum[kMaxL + 1];  // flattened fast-path tile offsets (wave-uniform)
+  {
+    const int gl = lane >> 4, gk = lane & 15;
+    const bool act = gl < L && gk < np;
+    const float xr = __shfl(cv, min(gk, np - 1), kWave), yr = __shfl(cv, np + min(gk, np - 1), kWave);
+    const float sc = lv.scale[gl < L ? gl : 0];
+    const bool pow2 = (__float_as_uint(sc) & 0x7fffffu) == 0u;  // x / 2^k == x * 2^-k
+    const float rs = 1.0f / sc;
+    const float x = pow2 ? xr * rs : xr / sc, y = pow2 ? yr * rs : yr / sc;
+    const int xf = ifloor_safe(x), yf = ifloor_safe(y);
+    if (act) {
+      geo[gl].x0[gk] = xf;
+      geo[gl].y0[gk] = yf;
+      geo[gl].dx[gk] = x - floorf(x);  // correlation_kernel.cu:262
+      geo[gl].dy[gk] = y - floorf(y);
+    }
+    int xlo = act ? xf : 0x7fffffff, ylo = act ? yf : 0x7fffffff;
+    int xhi = act ? xf : -0x7fffffff, yhi = act ? yf : -0x7fffffff;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      xlo = min(xlo, __shfl_xor(xlo, o, kWave));
+      ylo = min(ylo, __shfl_xor(ylo, o, kWave));
+      xhi = max(xhi, __shfl_xor(xhi, o, kWave));
+      yhi = max(yhi, __shfl_xor(yhi, o, kWave));
+    }
+    if (gk == 0 && gl < L) {
+      const int H2 = lv.H2[gl], W2 = lv.W2[gl];
+      xlo = max(xlo - R, 0);
+      ylo = max(ylo - R, 0);
+      xhi = min(xhi + R + 1, W2 - 1);
+      yhi = min(yhi + R + 1, H2 - 1);
+      int bw = xhi - xlo + 1, bh = yhi - ylo + 1;
+      if (bw <= 0 || bh <= 0 || !idx_ok) bw = bh = 0;
+      geo[gl].xlo = xlo;
+      geo[gl].ylo = ylo;
+      geo[gl].bw = bw;
+      geo[gl].bh = bh;
+      geo[gl].ntile = (bw * bh + 15) >> 4;
+    }
+  }
+  wave_lds_sync();  // geo visible, A fragments read (G free)
+  // Level order: the fine level streams from HBM / the Infinity Cache, the
+  // coarse levels hit in L2 and are matrix-core bound.  The second wave on a
+  // SIMD (hardware wave slot, HW_ID[3:0]) walks the levels coarse -> fine, so
+  // the two waves of a SIMD are in opposite phases instead of both waiting on
+  // memory first and both multiplying later.
+  const bool rev = (__builtin_amdgcn_s_getreg((3 << 11) | 4) & 1) != 0;
+  auto level_at = [&](int j) { return rev ? L - 1 - j : j; };  // position -> level
+  cum[0] = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxL; j++) {
+    const int nt = (j < L) ? wave_uniform(geo[level_at(j)].ntile) : 0;
+    cum[j + 1] = cum[j] + ((nt <= kMaxTiles) ? nt : 0);
+  }
+  CORR_STAMP(1);
+
+  // ---- per-lane output codes o = lane + 64u -> (k, yy, xx), once
+  int code[kOutPerLane];
+#pragma unroll
+  for (int u = 0; u < kOutPerLane; u++) {
+    const int o = lane + kWave * u;
+    const int k = o % np, t = o / np, yy = t % Dp, xx = t / Dp;
+    code[u] = (o < nout) ? (k | (yy << 8) | (xx << 16)) : -1;
+  }
   float outv[kOutPerLane][kMaxL];
-  for (int l = 0; l < L; l++) {
-    const int H2 = lv.H2[l], W2 = lv.W2[l];
-    // ---- geometry: coords [B,M,2,np] / scale -> floor / frac per patch pixel
-    float cv = 0.f;
-    if (lane < 2 * np) cv = coords[((size_t)b * M + m) * 2 * np + lane] / lv.scale[l];
-    int xlo = 0x7fffffff, xhi = -0x7fffffff, ylo = 0x7fffffff, yhi = -0x7fffffff;
 #pragma unroll
-    for (int k = 0; k < kNpMax; k++) {
-      if (k < np) {
-        const float x = __shfl(cv, k, kWave);
-        const float y = __shfl(cv, np + k, kWave);
-        const int xf = ifloor_safe(x), yf = ifloor_safe(y);
-        xlo = min(xlo, xf);
-        xhi = max(xhi, xf);
-        ylo = min(ylo, yf);
-        yhi = max(yhi, yf);
-        if (lane == 0) {
-          geo->x0[k] = xf;
-          geo->y0[k] = yf;
-          geo->dx[k] = x - floorf(x);  // correlation_kernel.cu:262
-          geo->dy[k] = y - floorf(y);
-        }
-      }
-    }
-    xlo = wave_uniform(max(xlo - R, 0));
-    ylo = wave_uniform(max(ylo - R, 0));
-    xhi = wave_uniform(min(xhi + R + 1, W2 - 1));
-    yhi = wave_uniform(min(yhi + R + 1, H2 - 1));
-    int bw = xhi - xlo + 1, bh = yhi - ylo + 1;
-    if (bw <= 0 || bh <= 0 || !idx_ok) bw = bh = 0;
-    const int npx = bw * bh, ntile = (npx + 15) >> 4;
-    const bool fast = ntile <= kMaxTiles;
-    const float* f2 = lv.f2[l] + ((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 * C;
-    wave_lds_sync();  // geo visible; previous level's G reads done
+  for (int u = 0; u < kOutPerLane; u++)
+#pragma unroll
+    for (int ll = 0; ll < kMaxL; ll++) outv[u][ll] = 0.f;
 
-    if (fast) {
-      // ---- G tile t: 16 box pixels x 128 channels, 8 x 16-B loads per lane
-      auto tile_src = [&](int t) -> const float* {
-        const int j = min(16 * t + ai, max(npx - 1, 0));  // pad columns read pixel npx-1
-        const int r = j / max(bw, 1), cc = j - r * max(bw, 1);
-        return f2 + ((size_t)(ylo + r) * W2 + xlo + cc) * C + 4 * aq;
-      };
-      float4 cur[8], nxt[8];
-      if (ntile > 0) {
-        const float* src = tile_src(0);
-#pragma unroll
-        for (int h = 0; h < 8; h++) cur[h] = *reinterpret_cast<const float4*>(src + 16 * h);
-      }
-      for (int t = 0; t < ntile; t++) {
-        if (t + 1 < ntile) {  // next tile in flight while this one multiplies
-          const float* src = tile_src(t + 1);
-#pragma unroll
-          for (int h = 0; h < 8; h++) nxt[h] = *reinterpret_cast<const float4*>(src + 16 * h);
-        }
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int h = 0; h < 8; h++) {
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 0], cur[h].x, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 1], cur[h].y, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 2], cur[h].z, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 3], cur[h].w, acc, 0, 0, 0);
-        }
-        // D: lane holds rows 4q + r (patch pixels), column lane & 15 (box pixel)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int row = 4 * aq + r;
-          if (row < np) G[row * kBoxStride + 16 * t + ai] = acc[r];
-        }
-#pragma unroll
-        for (int h = 0; h < 8; h++) cur[h] = nxt[h];
-      }
-    } else {
-      // ---- rare: windows too spread for the box: raw[k][yy][xx] directly
-      for (int e = lane; e < np * D * D; e += kWave) {
-        const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
-        const int i1 = geo->y0[k] + yy - R, j1 = geo->x0[k] + xx - R;
-        float s = 0.f;
-        if (i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
-          const float* px = f2 + ((size_t)i1 * W2 + j1) * C;
-          const float* f1 = fmap1 + ((size_t)b * N1 + ix) * C * np;
-          for (int c = 0; c < C; c++) s += f1[(size_t)c * np + k] * px[c];
-        }
-        G[e] = s;
-      }
-    }
-    wave_lds_sync();
-
-    // ---- bilinear + permute (correlation_kernel.cu:260-271) into registers
+  // bilinear + permute of level l from G (correlation_kernel.cu:260-271).
+  // Branch-free: every tap is loaded from a clamped (valid) LDS address and
+  // zeroed by a select, so the 32 LDS reads of a level issue back to back
+  // instead of one branch (and one LDS round trip) per tap.
+  auto bilinear = [&](int l, bool fast) {
+    const NhwcGeom* gg = geo + l;
+    const int xlo = wave_uniform(gg->xlo), ylo = wave_uniform(gg->ylo);
+    const int bw = wave_uniform(gg->bw), bh = wave_uniform(gg->bh);
+    const int cap = max(bw * bh - 1, 0);
 #pragma unroll
     for (int u = 0; u < kOutPerLane; u++) {
-      const int o = lane + kWave * u;
-      float v = 0.f;
-      if (o < nout) {
-        const int k = o % np, t = o / np, yy = t % Dp, xx = t / Dp;
-        float r00, r01, r10, r11;
-        if (fast) {
-          const int gy = geo->y0[k] + yy - R - ylo, gx = geo->x0[k] + xx - R - xlo;
-          const float* g = G + k * kBoxStride;
-          auto at = [&](int y, int x) -> float {
-            return (y >= 0 && y < bh && x >= 0 && x < bw) ? g[y * bw + x] : 0.f;
-          };
-          r00 = at(gy, gx);
-          r01 = at(gy, gx + 1);
-          r10 = at(gy + 1, gx);
-          r11 = at(gy + 1, gx + 1);
-        } else {
-          const float* g = G + k * D * D;
-          r00 = g[yy * D + xx];
-          r01 = g[yy * D + xx + 1];
-          r10 = g[(yy + 1) * D + xx];
-          r11 = g[(yy + 1) * D + xx + 1];
-        }
-        const float dx = geo->dx[k], dy = geo->dy[k];
-        v = ((1.f - dx) * (1.f - dy)) * r00;
-        v = v + (dx * (1.f - dy)) * r01;
-        v = v + ((1.f - dx) * dy) * r10;
-        v = v + (dx * dy) * r11;
+      const int cd = max(code[u], 0);
+      const int k = cd & 0xff, yy = (cd >> 8) & 0xff, xx = cd >> 16;
+      float r00, r01, r10, r11;
+      if (fast) {
+        const int gy = gg->y0[k] + yy - R - ylo, gx = gg->x0[k] + xx - R - xlo;
+        const float* g = G + k * kBoxStride;
+        const bool y0i = gy >= 0 && gy < bh, y1i = gy + 1 >= 0 && gy + 1 < bh;
+        const bool x0i = gx >= 0 && gx < bw, x1i = gx + 1 >= 0 && gx + 1 < bw;
+        const int i00 = min(max(gy * bw + gx, 0), cap);
+        const int i01 = min(max(gy * bw + gx + 1, 0), cap);
+        const int i10 = min(max((gy + 1) * bw + gx, 0), cap);
+        const int i11 = min(max((gy + 1) * bw + gx + 1, 0), cap);
+        const float a00 = g[i00], a01 = g[i01], a10 = g[i10], a11 = g[i11];
+        r00 = (y0i && x0i) ? a00 : 0.f;
+        r01 = (y0i && x1i) ? a01 : 0.f;
+        r10 = (y1i && x0i) ? a10 : 0.f;
+        r11 = (y1i && x1i) ? a11 : 0.f;
+      } else {
+        const float* g = G + k * D * D;
+        r00 = g[yy * D + xx];
+        r01 = g[yy * D + xx + 1];
+        r10 = g[(yy + 1) * D + xx];
+        r11 = g[(yy + 1) * D + xx + 1];
       }
+      const float dx = gg->dx[k], dy = gg->dy[k];
+      float v = ((1.f - dx) * (1.f - dy)) * r00;
+      v = v + (dx * (1.f - dy)) * r01;
+      v = v + ((1.f - dx) * dy) * r10;
+      v = v + (dx * dy) * r11;
+      v = (code[u] >= 0) ? v : 0.f;
 #pragma unroll
-      for (int ll = 0; ll < kMaxL; ll++)
-        if (ll == l) outv[u][ll] = v;
+      for (int ll = 0; ll < kMaxL; ll++) outv[u][ll] = (ll == l) ? v : outv[u][ll];
+    }
+  };
+
+  // levels off the fast path (empty box, or windows too spread for it) first
+  for (int l = 0; l < L; l++) {
+    const int nt = wave_uniform(geo[l].ntile);
+    if (nt > kMaxTiles) {  // raw[k][yy][xx] directly into G
+      const int H2 = lv.H2[l], W2 = lv.W2[l];
+      const float* f2 = lv.f2[l] + ((size_t)b * N2 + jx) * H2 * W2 * C;
+      for (int e = lane; e < np * D * D; e += kWave) {
+        const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
+        const int i1 = geo[l].y0[k] + yy - R, j1 = geo[l].x0[k] + xx - R;
+        float sacc = 0.f;
+        if (idx_ok && i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
+          const float* px = f2 + ((size_t)i1 * W2 + j1) * C;
+          const float* f1 = fmap1 + ((size_t)b * N1 + ix) * C * np;
+          for (int c = 0; c < C; c++) sacc += f1[(size_t)c * np + k] * px[c];
+        }
+        G[e] = sacc;
+      }
+      wave_lds_sync();
+      bilinear(l, false);
+      wave_lds_sync();
+    } else if (nt == 0) {
+      bilinear(l, true);  // every tap reads 0 (out of the empty box)
     }
   }
+
+  // ---- flattened fast-path tiles, kRing - 1 in flight
+  const int T = cum[L];
+  auto tile_src = [&](int i) -> const float* {
+    i = min(i, max(T - 1, 0));  // past the end: re-read the last tile (never used)
+    const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
+    const int t = i - (j == 0 ? 0 : j == 1 ? cum[1] : j == 2 ? cum[2] : cum[3]);
+    const int l = level_at(j);
+    const NhwcGeom* gg = geo + l;
+    const int bw0 = wave_uniform(gg->bw), npx = bw0 * wave_uniform(gg->bh);
+    const float rbw = 1.0f / (float)max(bw0, 1);
+    const int px = min(16 * t + ai, max(npx - 1, 0));  // pad columns read pixel npx-1
+    const int r = (int)(((float)px + 0.5f) * rbw), cc = px - r * max(bw0, 1);
+    const int H2 = lv.H2[l], W2 = lv.W2[l];
+    const float* f2 = lv.f2[l] + ((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 * C;
+    return f2 + ((size_t)(wave_uniform(gg->ylo) + r) * W2 + wave_uniform(gg->xlo) + cc) * C +
+           4 * aq;
+  };
+  if (T > 0) {
+    // register ring: cur = tile i, n1 / n2 = tiles i + 1, i + 2 in flight;
+    // one loop body (rotation by register moves, which issue in the MFMA
+    // shadow) keeps the kernel small enough for the instruction cache
+    float4 cur[8], n1[8], n2[8];
+    {
+      const float* s0 = tile_src(0);
+      const float* s1 = tile_src(1);
+      const float* s2 = tile_src(2);
+#pragma unroll
+      for (int h = 0; h < 8; h++) cur[h] = *reinterpret_cast<const float4*>(s0 + 16 * h);
+#pragma unroll
+      for (int h = 0; h < 8; h++) n1[h] = *reinterpret_cast<const float4*>(s1 + 16 * h);
+#pragma unroll
+      for (int h = 0; h < 8; h++) n2[h] = *reinterpret_cast<const float4*>(s2 + 16 * h);
+    }
+    for (int i = 0; i < T; i++) {
+      // two accumulators (even / odd channel groups): two independent MFMA
+      // chains, summed once per tile in a fixed order
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < 8; h += 2) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 0], cur[h].x, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 4], cur[h + 1].x, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 1], cur[h].y, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 5], cur[h + 1].y, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 2], cur[h].z, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 6], cur[h + 1].z, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 3], cur[h].w, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 7], cur[h + 1].w, acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int h = 0; h < 8; h++) {
+        cur[h] = n1[h];
+        n1[h] = n2[h];
+      }
+      {  // tile i + 3 (past the end: the last tile again, never used)
+        const float* src = tile_src(i + 3);
+#pragma unroll
+        for (int h = 0; h < 8; h++) n2[h] = *reinterpret_cast<const float4*>(src + 16 * h);
+      }
+      const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
+      const int lb = (j == 0 ? 0 : j == 1 ? cum[1] : j == 2 ? cum[2] : cum[3]);
+      const int t = i - lb, l = level_at(j);
+      // D: lane holds rows 4q + r (patch pixels), column lane & 15 (box pixel)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = 4 * aq + r;
+        if (row < np) G[row * kBoxStride + 16 * t + ai] = acc0[r] + acc1[r];
+      }
+      const int le = (j == 0 ? cum[1] : j == 1 ? cum[2] : j == 2 ? cum[3] : cum[4]);
+      if (i + 1 == le) {  // level complete: bilinear, then G is free again
+        wave_lds_sync();
+        CORR_STAMP(2 + 2 * l);
+        bilinear(l, true);
+        wave_lds_sync();
+        CORR_STAMP(3 + 2 * l);
+      }
+    }
+  }
+
   // ---- one contiguous [nout][L] row block per edge
+  CORR_STAMP(10);
   float* dst = out + ((size_t)b * M + m) * nout * L;
 #pragma unroll
   for (int u = 0; u < kOutPerLane; u++) {
@@ -213,6 +367,8 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave)
         if (ll < L) dst[(size_t)o * L + ll] = outv[u][ll];
     }
   }
+  CORR_STAMP(11);
+  CORR_STAMP_RT(13);
 }
 
 // [count, C, H, W] -> [count, H, W, C] (one 32 x 32 tile of (c, hw) per block)
@@ -360,12 +516,10 @@ __global__ void __launch_bounds__(256)
 
 using namespace dpvo;
 
-DPVO_EXPORT int dpvo_corr_forward_levels_nhwc(const void* fmap1, const void* const* fmap2,
-                                              const int* H2, const int* W2, const float* scale,
-                                              int L, const float* coords, const int64_t* ii,
-                                              const int64_t* jj, int B, int M, int C, int H,
-                                              int W, int N1, int N2, int radius, int dtype,
-                                              float* out, void* stream) {
+DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
+    const void* fmap1, const void* const* fmap2, const int* H2, const int* W2, const float* scale,
+    int L, const float* coords, const int64_t* ii, const int64_t* jj, const int32_t* order, int B,
+    int M, int C, int H, int W, int N1, int N2, int radius, int dtype, float* out, void* stream) {
   if (L <= 0 || radius < 0 || radius > 7 || C <= 0 || H <= 0 || W <= 0) return DPVO_ERR_INVALID;
   const int np = H * W, Dp = 2 * radius + 1;
   if (dtype != DPVO_F32 || C != kNhwcC || L > kMaxL || np > kNpMax ||
@@ -381,12 +535,31 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc(const void* fmap1, const void* con
     lv.W2[l] = W2[l];
     lv.scale[l] = scale[l];
   }
-  const size_t smem = sizeof(float) * kNhwcWaves * kNpMax * kBoxStride +
-                      sizeof(NhwcGeom) * kNhwcWaves;
-  hipLaunchKernelGGL(corr_nhwc_kernel, dim3((B * M + kNhwcWaves - 1) / kNhwcWaves),
-                     dim3(kNhwcWaves * kWave), smem, as_stream(stream), (const float*)fmap1, lv,
-                     L, coords, ii, jj, B, M, np, N1, N2, radius, out);
+  // G: np rows x kBoxStride per wave (the slow path's np x D x D fits too:
+  // D * D <= 256 > kBoxStride only for R > 5, which the fast path covers)
+  const int D = 2 * radius + 2;
+  if (D * D > kBoxStride) return DPVO_ERR_UNSUPPORTED;
+  const size_t smem = sizeof(float) * kNhwcWaves * np * kBoxStride +
+                      sizeof(NhwcGeom) * kNhwcWaves * kMaxL;
+  const long long units = (long long)B * M;
+  unsigned grid = (unsigned)((units + kNhwcWaves - 1) / kNhwcWaves);
+  const bool ordered = order && B == 1;
+  if (ordered) grid = 8u * (unsigned)((grid + 7) / 8);
+  hipLaunchKernelGGL(corr_nhwc_kernel, dim3(grid), dim3(kNhwcWaves * kWave), smem,
+                     as_stream(stream), (const float*)fmap1, lv, L, coords, ii, jj, B, M, np, N1,
+                     N2, radius, ordered ? (const int*)order : (const int*)nullptr, out);
   return launch_status();
+}
+
+DPVO_EXPORT int dpvo_corr_forward_levels_nhwc(const void* fmap1, const void* const* fmap2,
+                                              const int* H2, const int* W2, const float* scale,
+                                              int L, const float* coords, const int64_t* ii,
+                                              const int64_t* jj, int B, int M, int C, int H,
+                                              int W, int N1, int N2, int radius, int dtype,
+                                              float* out, void* stream) {
+  return dpvo_corr_forward_levels_nhwc_ordered(fmap1, fmap2, H2, W2, scale, L, coords, ii, jj,
+                                               nullptr, B, M, C, H, W, N1, N2, radius, dtype, out,
+                                               stream);
 }
 
 DPVO_EXPORT int dpvo_feature_to_nhwc(const void* src, void* dst, int count, int C, int H, int W,

@@ -93,7 +93,8 @@ void feature_pyramid_insert(torch::Tensor src, std::vector<torch::Tensor> dst,
 
 torch::Tensor corr_forward_levels(torch::Tensor fmap1, std::vector<torch::Tensor> fmap2,
                                   torch::Tensor coords, torch::Tensor ii, torch::Tensor jj,
-                                  int radius, std::vector<double> scales) {
+                                  int radius, std::vector<double> scales,
+                                  c10::optional<torch::Tensor> order) {
   check_device(fmap1, "fmap1");
   TORCH_CHECK(fmap2.size() == scales.size() && !fmap2.empty() && fmap2.size() <= 8,
               "one scale per pyramid level (1..8 levels)");
@@ -123,9 +124,17 @@ torch::Tensor corr_forward_levels(torch::Tensor fmap1, std::vector<torch::Tensor
   }
   if (nhwc) {
     for (int l = 0; l < L; l++) ptrs[l] = fmap2[l].data_ptr();
-    const int st = dpvo_corr_forward_levels_nhwc(
+    const int32_t* ord = nullptr;
+    if (order.has_value() && order->defined()) {
+      check_device(*order, "order");
+      TORCH_CHECK(order->scalar_type() == torch::kInt32 && order->is_contiguous() &&
+                      order->numel() == M && B == 1,
+                  "order: contiguous int32 [E] (B == 1)");
+      ord = order->data_ptr<int32_t>();
+    }
+    const int st = dpvo_corr_forward_levels_nhwc_ordered(
         fmap1.data_ptr(), ptrs.data(), H2.data(), W2.data(), sc.data(), L,
-        coords.data_ptr<float>(), ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), B, M,
+        coords.data_ptr<float>(), ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), ord, B, M,
         fmap1.size(2), H, W, fmap1.size(1), fmap2[0].size(1), radius, dtype_code(fmap1),
         out.data_ptr<float>(), current_stream());
     if (st != DPVO_ERR_UNSUPPORTED) {
@@ -236,7 +245,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("patchify_forward", &patchify_forward, "PATCHIFY forward");
   m.def("patchify_backward", &patchify_backward, "PATCHIFY backward");
   // additions (not in the reference surface)
-  m.def("forward_levels", &corr_forward_levels, "CORR forward, all pyramid levels in one launch");
+  m.def("forward_levels", &corr_forward_levels, "CORR forward, all pyramid levels in one launch",
+        py::arg("fmap1"), py::arg("fmap2"), py::arg("coords"), py::arg("ii"), py::arg("jj"),
+        py::arg("radius"), py::arg("scales"), py::arg("order") = py::none());
   m.def("feature_pyramid_insert", &feature_pyramid_insert,
         "NCHW level-1 frame -> channels-last pyramid slot (all levels, one launch)");
   m.def("feature_to_nhwc", &feature_to_nhwc, "[..., C, H, W] -> channels-last copy into dst");

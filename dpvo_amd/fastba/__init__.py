@@ -30,9 +30,14 @@ def neighbors(ii, jj):
     return cuda_ba.neighbors(ii, jj)
 
 
-def reproject(poses, patches, intrinsics, ii, jj, kk):
-    """cuda_ba.reproject (ba_cuda.cu:379-429, 585-616)."""
-    return cuda_ba.reproject(poses, patches, intrinsics, ii, jj, kk)
+def reproject(poses, patches, intrinsics, ii, jj, kk, mem=None):
+    """cuda_ba.reproject (ba_cuda.cu:379-429, 585-616).  With ``mem`` (the
+    feature ring size the targets jj index), also returns the A-CORR edge
+    order (int32 [E], edges grouped by target frame) computed in the same
+    launch: ``coords, order = reproject(..., mem=36)``."""
+    if mem is None:
+        return cuda_ba.reproject(poses, patches, intrinsics, ii, jj, kk)
+    return tuple(cuda_ba.reproject_ordered(poses, patches, intrinsics, ii, jj, kk, int(mem)))
 
 
 __all__ = ["BA", "neighbors", "reproject", "cuda_ba"]

@@ -79,6 +79,17 @@ int dpvo_corr_forward_levels_nhwc(const void* fmap1, const void* const* fmap2, c
                                   const int64_t* ii, const int64_t* jj, int B, int M, int C,
                                   int H, int W, int N1, int N2, int radius, int dtype, float* out,
                                   void* stream);
+/* The same with an edge order (B == 1): order[p] = edge processed at position
+   p, as written by dpvo_reproject_ordered (edges grouped by target frame).
+   Workgroups are mapped to XCDs so that each XCD processes one contiguous
+   eighth of that order: a target frame's pyramid levels stay in one XCD's L2.
+   Results are identical to the unordered call (order == NULL). */
+int dpvo_corr_forward_levels_nhwc_ordered(const void* fmap1, const void* const* fmap2,
+                                          const int* H2, const int* W2, const float* scale, int L,
+                                          const float* coords, const int64_t* ii,
+                                          const int64_t* jj, const int32_t* order, int B, int M,
+                                          int C, int H, int W, int N1, int N2, int radius,
+                                          int dtype, float* out, void* stream);
 /* Feature maps [count,C,H,W] -> channels-last [count,H,W,C] (the per-frame
    cost of keeping a channels-last pyramid; dtype F32 or F16). */
 int dpvo_feature_to_nhwc(const void* src, void* dst, int count, int C, int H, int W, int dtype,
@@ -130,6 +141,13 @@ size_t dpvo_ba_workspace_bytes(int E, int t0, int t1);
    2 = the multi-kernel path; 3 = same as 0; 4 = always the large-graph path.
    Process-wide; call before sizing the workspace. */
 int dpvo_ba_select_path(int mode);
+
+/* Dense pose solve of the default (blocks) path.  mode 2 (default): fp64
+   block LDL^T with a look-ahead pivot factorisation; 0: fp32 blocked Cholesky
+   (the reference's own precision, ba_cuda.cu:547-548); 1: fp32 Cholesky plus
+   one fp64 iterative-refinement step.  Measured on cfg2 (N = 11): 21 / 24 /
+   37 us per iteration for modes 2 / 0 / 1.  Process-wide. */
+int dpvo_ba_set_refine(int on);
 
 /* Largest number of free poses (t1 - t0) dpvo_ba_forward handles. */
 int dpvo_ba_max_free_poses(void);
@@ -218,6 +236,15 @@ int dpvo_gba_info(const void* workspace, int E, int t0, int t1, int* out, void* 
 int dpvo_reproject(const float* poses, const float* patches, const float* intrinsics,
                    const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int P,
                    int num_poses, int num_patches, float* coords, void* stream);
+
+/* dpvo_reproject plus, in the same launch (one extra workgroup), the A-CORR
+   edge order: order[0..E) = edges grouped by target frame jj (jj in [0, N2);
+   keys outside share the last group).  Feeds
+   dpvo_corr_forward_levels_nhwc_ordered. */
+int dpvo_reproject_ordered(const float* poses, const float* patches, const float* intrinsics,
+                           const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int P,
+                           int num_poses, int num_patches, int N2, float* coords, int32_t* order,
+                           void* stream);
 
 /* F-NBR.  Replaces cuda_ba.neighbors (ba.cpp:59-97).  Groups edges by ii,
    stable-sorts each group by jj; ix = previous edge, jx = next edge, -1 at

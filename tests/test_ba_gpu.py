@@ -256,3 +256,22 @@ def test_fused_general_graph_structure(cb, gpu, path, seed):
     P, K = _run_gpu(cb, G, gpu, 2, G.F - 1, 2)
     Pr, Kr = _run_oracle(G, 2, G.F - 1, 2)
     _check(P, K, Pr, Kr)
+
+
+@pytest.mark.parametrize("refine", [0, 1, 2], ids=["fp32-solve", "fp32+fp64-refine", "fp64-ldl"])
+def test_blocks_solve_precision(cb, gpu, refine):
+    """The blocks path's dense solve modes -- fp32 Cholesky (the reference's
+    precision), fp32 + one fp64 refinement step, fp64 block LDL^T (the
+    default) -- all stay within the north_star tolerances of the fp64 oracle
+    on cfg2 (condition numbers ~2e5)."""
+    cb.set_refine(refine)
+    try:
+        for seed in (0, 4):
+            G = synthetic.make_config("cfg2", seed=seed)
+            P, K = _run_gpu(cb, G, gpu, 1, G.F, 2)
+            Pr, Kr = _run_oracle(G, 1, G.F, 2)
+            _check(P, K, Pr, Kr)
+            if refine:  # fp64-level solves: the oracle's up to the fp32 edge math
+                np.testing.assert_allclose(P, Pr, rtol=0, atol=2e-6)
+    finally:
+        cb.set_refine(2)

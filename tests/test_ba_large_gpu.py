@@ -146,7 +146,9 @@ def test_cfg4_full_size_runs_and_agrees_with_sharded(cb, gpu):
     t0, t1 = 1, G.F
     ws, D, info = _info(cb, G, gpu, t0, t1)
     status, nuniq, nitems, nblk, nI, nB, g, nsb = info
-    assert status == 0 and nuniq == G.F * G.M and nB <= 10 and g <= 16
+    # the recipe gives every patch of frames < F-1 an edge to frame
+    # i+1; the last frame's patches are covered only by the random edges
+    assert status == 0 and nuniq == len(np.unique(G.kk.numpy())) and nB <= 10 and g <= 16
     P1, K1 = _gpu(cb, G, gpu, t0, t1, 2)
     P2, K2 = _gpu(cb, G, gpu, t0, t1, 2)
     np.testing.assert_array_equal(P1, P2)
