@@ -29,6 +29,19 @@ sys.path.insert(0, REPO)
 
 METRIC = "update-iterations/sec (altcorr+fastba) on 96-patch/2048-edge graph, 1→8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                            "profiles", "r01_corr_traffic.json")
+
+
+def pmc_traffic(config):
+    """Per-launch HBM bytes of corr_nhwc_kernel from the committed PMC passes
+    (scripts/pmc.sh + scripts/traffic_summary.py; FETCH_SIZE doubled per the
+    gfx950 correction). Counters cannot be read live inside the timed run, so
+    the figure is only reported for the default cfg2 workload it was taken on."""
+    if config != "cfg2" or not os.path.exists(TRAFFIC_FILE):
+        return None
+    with open(TRAFFIC_FILE) as f:
+        return json.load(f)["traffic_bytes_per_launch"]
 
 
 def algorithmic_corr_bytes(coords, H2s, W2s, scales, C, p, R, feat_bytes):
@@ -230,7 +243,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": pmc_traffic(args.config),
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "kernel_ms": corr_ms,
                 "per_level": per_level,
