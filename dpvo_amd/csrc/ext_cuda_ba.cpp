@@ -151,13 +151,48 @@ std::vector<torch::Tensor> ba_neighbors(torch::Tensor ii, torch::Tensor jj) {
   return {ix, jx};
 }
 
-// ba.cpp:120-180: Sim3 pose-graph solve of the loop-closure backend.
-std::vector<torch::Tensor> ba_solve_system(torch::Tensor, torch::Tensor, torch::Tensor,
-                                           torch::Tensor, torch::Tensor, double, double, int) {
-  TORCH_CHECK(false,
-              "cuda_ba.solve_system (loop-closure pose graph, dpvo/fastba/ba.cpp:120-180) is not "
-              "part of this build (SURVEY 8f rank 2)");
-  return {};
+// ba.cpp:120-180: Sim3 pose-graph solve of the loop-closure backend
+// (optim_utils.py:229).  Assembly of A = J^T J (+ damping) and b = -J^T res on
+// the device (pgo.hip, fp64 like the reference's Eigen system); the SPD solve of
+// the top-left freen*7 block by the device Cholesky in fp64; delta returned as
+// f32 [n, 7] with the rows of fixed poses zero (ba.cpp:103-118).
+std::vector<torch::Tensor> ba_solve_system(torch::Tensor J_Ginv_i, torch::Tensor J_Ginv_j,
+                                           torch::Tensor ii, torch::Tensor jj, torch::Tensor res,
+                                           double ep, double lm, int freen) {
+  check_device(res, "res");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(res.device());
+  J_Ginv_i = f32_contig(J_Ginv_i, "J_Ginv_i");
+  J_Ginv_j = f32_contig(J_Ginv_j, "J_Ginv_j");
+  res = f32_contig(res, "res");
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  const int64_t r = res.size(0);
+  TORCH_CHECK(r > 0 && res.numel() == 7 * r, "res must be [r, 7] with r > 0");
+  TORCH_CHECK(J_Ginv_i.numel() == 49 * r && J_Ginv_j.numel() == 49 * r,
+              "J_Ginv_i / J_Ginv_j must be [r, 7, 7]");
+  TORCH_CHECK(ii.numel() == r && jj.numel() == r, "ii / jj must be [r]");
+  // the reference calls exit(1) on a self edge (ba.cpp:150-151); raise instead
+  TORCH_CHECK(!(ii == jj).any().item<bool>(), "cuda_ba.solve_system: edge with ii == jj");
+  TORCH_CHECK(ii.min().item<int64_t>() >= 0 && jj.min().item<int64_t>() >= 0,
+              "cuda_ba.solve_system: negative pose index");
+  const int64_t n = std::max(ii.max().item<int64_t>(), jj.max().item<int64_t>()) + 1;
+  const auto opt64 = res.options().dtype(torch::kFloat64);
+  auto A = torch::empty({7 * n, 7 * n}, opt64);
+  auto b = torch::empty({7 * n}, opt64);
+  check_status(dpvo_pgo_assemble(J_Ginv_i.data_ptr<float>(), J_Ginv_j.data_ptr<float>(),
+                                 ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(),
+                                 res.data_ptr<float>(), (int)r, (int)n, (float)ep, (float)lm,
+                                 A.data_ptr<double>(), b.data_ptr<double>(), current_stream()),
+               "cuda_ba.solve_system");
+  int64_t f = (int64_t)freen * 7;  // solve(A, b, freen*7): < 0 -> whole system
+  if (f < 0 || f > 7 * n) f = 7 * n;
+  auto delta = torch::zeros({7 * n}, opt64);
+  if (f > 0) {
+    auto As = A.narrow(0, 0, f).narrow(1, 0, f);
+    auto L = std::get<0>(at::linalg_cholesky_ex(As));
+    delta.narrow(0, 0, f).copy_(at::cholesky_solve(b.narrow(0, 0, f).unsqueeze(1), L).squeeze(1));
+  }
+  return {delta.to(torch::kFloat32).view({n, 7})};
 }
 
 // Split F-BA for the edge-sharded multi-GPU path.
@@ -302,7 +337,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("forward", &ba_forward, "BA forward operator");
   m.def("neighbors", &ba_neighbors, "temporal neighboor indicies");
   m.def("reproject", &ba_reproject, "temporal neighboor indicies");
-  m.def("solve_system", &ba_solve_system, "temporal neighboor indicies");
+  m.def("solve_system", &ba_solve_system, "Sim3 pose-graph solve (ba.cpp:120-180)");
   // additions: split BA for the sharded multi-GPU path
   m.def("setup", &ba_setup, "BA graph setup -> workspace");
   m.def("build_schur", &ba_build_schur, "linearize + Schur complement (S_lower, y)");

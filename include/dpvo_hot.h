@@ -149,6 +149,16 @@ int dpvo_ba_select_path(int mode);
    37 us per iteration for modes 2 / 0 / 1.  Process-wide. */
 int dpvo_ba_set_refine(int on);
 
+/* Sim3 pose-graph normal equations.  Replaces the host assembly of
+   cuda_ba.solve_system (dpvo/fastba/ba.cpp:120-165): J_Ginv_i / J_Ginv_j
+   [r, 7, 7] f32, ii / jj [r] int64 (ii != jj, < n), res [r, 7] f32 ->
+   dense A [7n, 7n] = J^T J with diag(A) += diag(A)*lm + ep, and
+   b [7n] = -J^T res, both fp64 (device memory, zeroed here).  The Cholesky
+   solve of the top-left freen*7 block runs in the caller (ba.cpp:103-118). */
+int dpvo_pgo_assemble(const float* J_Ginv_i, const float* J_Ginv_j, const int64_t* ii,
+                      const int64_t* jj, const float* res, int r, int n, float ep, float lm,
+                      double* A, double* b, void* stream);
+
 /* Largest number of free poses (t1 - t0) dpvo_ba_forward handles. */
 int dpvo_ba_max_free_poses(void);
 

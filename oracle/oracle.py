@@ -242,3 +242,42 @@ def ba_shard(phase, poses, patches, intrinsics, target, weight, lmbda, ii, jj, k
     if phase == 1:
         return S[:36 * N * N].reshape(6 * N, 6 * N), y[:6 * N]
     return poses, patches
+
+
+def solve_system(J_Ginv_i, J_Ginv_j, ii, jj, res, ep, lm, freen):
+    """cuda_ba.solve_system (dpvo/fastba/ba.cpp:120-180), restated in numpy.
+
+    J [7r, 7n] from the per-edge blocks (ba.cpp:141-158), b = -J^T res and
+    A = J^T J in fp64 (160-163), diag(A) += diag(A)*lm, += ep (164-165), with
+    ep/lm rounded to fp32 as the pybind signature does; SPD solve of the
+    top-left freen*7 block, zero elsewhere (103-118); delta cast to fp32.
+    Parity unpinned: the reference needs Eigen (absent here) and its tests
+    hold no fixture for this op, so this restatement is the only anchor.
+    Poses with no edge get ep on the diagonal here; Eigen's sparse
+    ``diagonal()`` has no entry there (reference behaviour undefined)."""
+    Ji = np.asarray(J_Ginv_i, np.float32).astype(np.float64)
+    Jj = np.asarray(J_Ginv_j, np.float32).astype(np.float64)
+    ii = np.asarray(ii, np.int64)
+    jj = np.asarray(jj, np.int64)
+    v = np.asarray(res, np.float32).reshape(-1).astype(np.float64)
+    r = len(ii)
+    if np.any(ii == jj):
+        raise ValueError("edge with ii == jj (ba.cpp:150-151 exits)")
+    n = int(max(ii.max(), jj.max())) + 1
+    J = np.zeros((7 * r, 7 * n))
+    for x in range(r):
+        J[7 * x:7 * x + 7, 7 * ii[x]:7 * ii[x] + 7] = Ji[x]
+        J[7 * x:7 * x + 7, 7 * jj[x]:7 * jj[x] + 7] = Jj[x]
+    b = -(J.T @ v)
+    A = J.T @ J
+    d = np.diag(A).copy()
+    A[np.diag_indices_from(A)] = (d + d * float(np.float32(lm))) + float(np.float32(ep))
+    f = freen * 7
+    if f < 0 or f > 7 * n:
+        f = 7 * n
+    delta = np.zeros(7 * n)
+    if f > 0:
+        L = np.linalg.cholesky(A[:f, :f])
+        y = np.linalg.solve(L, b[:f])
+        delta[:f] = np.linalg.solve(L.T, y)
+    return delta.astype(np.float32).reshape(n, 7)
