@@ -172,10 +172,15 @@ std::vector<torch::Tensor> ba_solve_system(torch::Tensor J_Ginv_i, torch::Tensor
               "J_Ginv_i / J_Ginv_j must be [r, 7, 7]");
   TORCH_CHECK(ii.numel() == r && jj.numel() == r, "ii / jj must be [r]");
   // the reference calls exit(1) on a self edge (ba.cpp:150-151); raise instead
-  TORCH_CHECK(!(ii == jj).any().item<bool>(), "cuda_ba.solve_system: edge with ii == jj");
-  TORCH_CHECK(ii.min().item<int64_t>() >= 0 && jj.min().item<int64_t>() >= 0,
-              "cuda_ba.solve_system: negative pose index");
-  const int64_t n = std::max(ii.max().item<int64_t>(), jj.max().item<int64_t>()) + 1;
+  // one device->host sync for all index checks (the reference syncs on ii.max())
+  const auto st = torch::stack({(ii == jj).any().to(torch::kInt64),
+                                torch::minimum(ii.min(), jj.min()),
+                                torch::maximum(ii.max(), jj.max())})
+                      .cpu();
+  const int64_t* sv = st.data_ptr<int64_t>();
+  TORCH_CHECK(sv[0] == 0, "cuda_ba.solve_system: edge with ii == jj");
+  TORCH_CHECK(sv[1] >= 0, "cuda_ba.solve_system: negative pose index");
+  const int64_t n = sv[2] + 1;
   const auto opt64 = res.options().dtype(torch::kFloat64);
   auto A = torch::empty({7 * n, 7 * n}, opt64);
   auto b = torch::empty({7 * n}, opt64);
