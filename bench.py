@@ -193,6 +193,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
+    # every BA call of the run (warmup, event steps, graph replays) finished
+    # without a fatal status (raises RuntimeError otherwise)
+    ba_status = fastba.cuda_ba.check_status(poses)
+
     if world > 1:
         t = torch.tensor([elapsed, corr_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -249,6 +253,7 @@ def main():
                 "per_level": per_level,
             },
             "cpu_baseline": cpu,
+            "ba_status": ba_status,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

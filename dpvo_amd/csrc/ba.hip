@@ -1250,6 +1250,27 @@ DPVO_EXPORT int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1
              : DPVO_ERR_LAUNCH;
 }
 
+namespace dpvo {
+int gba_status_or(const void* workspace, int E, int N, int* acc, void* stream);
+}
+namespace {
+__global__ void k_status_or(const int* src, int* acc) {
+  if (threadIdx.x == 0) atomicOr(acc, *src);
+}
+}  // namespace
+
+DPVO_EXPORT int dpvo_ba_status_accumulate(const void* workspace, int E, int t0, int t1, int* acc,
+                                          void* stream) {
+  if (!workspace || !acc) return DPVO_ERR_INVALID;
+  if (E <= 0) return DPVO_OK;
+  const int N = t1 > t0 ? t1 - t0 : 0;
+  if (use_large(E, N)) return gba_status_or(workspace, E, N, acc, stream);
+  BaWs w;
+  ba_layout(E, N, (char*)workspace, &w);
+  hipLaunchKernelGGL(k_status_or, dim3(1), dim3(64), 0, as_stream(stream), w.meta + 1, acc);
+  return launch_status();
+}
+
 DPVO_EXPORT int dpvo_ba_phase_marks(const void* workspace, int E, int t0, int t1, int64_t* out,
                                     void* stream) {
   if (!workspace || !out || E <= 0) return DPVO_ERR_INVALID;

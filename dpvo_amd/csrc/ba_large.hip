@@ -973,6 +973,10 @@ __global__ void k_status_out(const Ws w, int* out) {
   }
 }
 
+__global__ void k_status_or_out(const Ws w, int* acc) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) atomicOr(acc, w.meta->status);
+}
+
 __global__ void k_clear_chol(Ws w) {
   if (threadIdx.x == 0 && blockIdx.x == 0) w.meta->status &= ~kStChol;
 }
@@ -1120,6 +1124,13 @@ int gba_solve_update(float* poses, float* patches, int E, int P, int t0, int t1,
   }
   hipLaunchKernelGGL(k_update, dim3(grid_of((long long)N + E)), dim3(kT), 0, s, poses, patches, E,
                      P, t0, N, w);
+  return launch_status();
+}
+
+int gba_status_or(const void* workspace, int E, int N, int* acc, void* stream) {
+  Ws w;
+  layout(E, N, (char*)workspace, &w);
+  hipLaunchKernelGGL(k_status_or_out, dim3(1), dim3(64), 0, as_stream(stream), w, acc);
   return launch_status();
 }
 

@@ -14,6 +14,13 @@ inline void* current_stream() {
   return reinterpret_cast<void*>(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream());
 }
 
+// true while the current stream is being captured into a hipGraph
+inline bool is_capturing() {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(), &cs);
+  return cs != hipStreamCaptureStatusNone;
+}
+
 inline void check_status(int st, const char* what) {
   TORCH_CHECK(st == DPVO_OK, what, " failed: ", dpvo_status_string(st), " (status ", st, ")");
 }

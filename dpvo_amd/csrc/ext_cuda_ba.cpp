@@ -1,5 +1,9 @@
 // ext_cuda_ba.cpp -- the `cuda_ba` extension module (drop-in for
 // dpvo/fastba/ba.cpp:183-189), bound to the C ABI in dpvo_hot.h.
+#include <map>
+#include <mutex>
+#include <string>
+
 #include "ext_common.hpp"
 
 using namespace dpvo_ext;
@@ -11,6 +15,118 @@ static torch::Tensor f32_contig(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32, got ",
               t.scalar_type());
   return t.contiguous();
+}
+
+// ---------------------------------------------------------------------------
+// BA status surfacing.  Every forward ORs its status word into a sticky
+// device int (one tiny kernel: graph-capturable, no sync) and, outside graph
+// capture, copies it asynchronously to pinned host memory.  The next forward
+// (or check_status()) reads a completed copy and raises RuntimeError when a
+// fatal bit is set: 2 kk out of range, 4 / 8 large-graph structure limits,
+// 16 cross-workgroup timeout (a dX = 0 step that the reference would not take).
+// Bit 1 (Cholesky failed -> zero step, dpvo/ba.py:17-21) is recorded, not
+// raised (the reference ignores `info`, ba_cuda.cu:547).  Errors therefore
+// surface at most one call late, like an asynchronous HIP error.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kFatalBits = 2 | 4 | 8 | 16;
+struct StatusSlot {
+  torch::Tensor acc;     // device int32 [1], sticky OR of all statuses
+  int* host = nullptr;   // pinned copy
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+  int last = 0;          // last status seen on the host (all bits)
+};
+std::mutex g_st_mu;
+std::map<int, StatusSlot> g_st;
+
+std::string describe_status(int s) {
+  std::string m;
+  if (s & 1) m += " [1: Cholesky failed, zero step]";
+  if (s & 2) m += " [2: kk outside [0, num_patches)]";
+  if (s & 4) m += " [4: a patch touches more free poses than the large-graph solver handles]";
+  if (s & 8) m += " [8: too many border poses for the large-graph solver]";
+  if (s & 16) m += " [16: cross-workgroup wait timed out]";
+  return m;
+}
+
+// consume a finished copy; raise on fatal bits (and reset the accumulator)
+void consume(StatusSlot& sl, bool wait, void* stream) {
+  if (!sl.pending) return;
+  if (wait) {
+    (void)hipEventSynchronize(sl.ev);
+  } else if (hipEventQuery(sl.ev) != hipSuccess) {
+    return;
+  }
+  sl.pending = false;
+  sl.last = *sl.host;
+  if (sl.last & kFatalBits) {
+    const int s = sl.last;
+    (void)hipMemsetAsync(sl.acc.data_ptr<int>(), 0, sizeof(int), (hipStream_t)stream);
+    *sl.host = 0;
+    TORCH_CHECK(false, "cuda_ba.forward: bundle adjustment reported status ", s,
+                describe_status(s), "; the poses/patches of that call did not take the "
+                "reference's step");
+  }
+}
+
+StatusSlot& slot_for(const torch::Tensor& like) {
+  const int dev = like.get_device();
+  auto& sl = g_st[dev];
+  if (!sl.acc.defined() && !is_capturing()) {
+    sl.acc = torch::zeros({1}, like.options().dtype(torch::kInt32));
+    TORCH_CHECK(hipHostMalloc((void**)&sl.host, sizeof(int), hipHostMallocDefault) == hipSuccess,
+                "cuda_ba: pinned status buffer");
+    *sl.host = 0;
+    TORCH_CHECK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) == hipSuccess,
+                "cuda_ba: status event");
+  }
+  return sl;
+}
+
+void track_status(const torch::Tensor& ws, const torch::Tensor& like, int E, int t0, int t1) {
+  std::lock_guard<std::mutex> lk(g_st_mu);
+  auto& sl = slot_for(like);
+  if (!sl.acc.defined()) return;  // first call happened inside a capture: untracked
+  void* st = current_stream();
+  check_status(dpvo_ba_status_accumulate(ws.data_ptr(), E, t0, t1, sl.acc.data_ptr<int>(), st),
+               "cuda_ba.forward(status)");
+  if (is_capturing() || sl.pending) return;
+  TORCH_CHECK(hipMemcpyAsync(sl.host, sl.acc.data_ptr<int>(), sizeof(int), hipMemcpyDeviceToHost,
+                             (hipStream_t)st) == hipSuccess, "cuda_ba: status copy");
+  TORCH_CHECK(hipEventRecord(sl.ev, (hipStream_t)st) == hipSuccess, "cuda_ba: status event");
+  sl.pending = true;
+}
+
+void poll_status(const torch::Tensor& like) {
+  if (is_capturing()) return;
+  std::lock_guard<std::mutex> lk(g_st_mu);
+  auto it = g_st.find(like.get_device());
+  if (it != g_st.end()) consume(it->second, false, current_stream());
+}
+}  // namespace
+
+// cuda_ba.check_status(device): synchronise on the status of every forward
+// issued so far on that device; raise on a fatal bit; return the OR of all
+// bits seen (bit 1 included) and reset the accumulator.
+int ba_check_status(torch::Tensor like) {
+  TORCH_CHECK(!is_capturing(), "cuda_ba.check_status: not allowed during graph capture");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(like.device());
+  std::lock_guard<std::mutex> lk(g_st_mu);
+  auto it = g_st.find(like.get_device());
+  if (it == g_st.end() || !it->second.acc.defined()) return 0;
+  auto& sl = it->second;
+  void* st = current_stream();
+  consume(sl, true, st);  // may raise
+  TORCH_CHECK(hipMemcpyAsync(sl.host, sl.acc.data_ptr<int>(), sizeof(int), hipMemcpyDeviceToHost,
+                             (hipStream_t)st) == hipSuccess, "cuda_ba: status copy");
+  TORCH_CHECK(hipEventRecord(sl.ev, (hipStream_t)st) == hipSuccess, "cuda_ba: status event");
+  sl.pending = true;
+  consume(sl, true, st);  // may raise
+  const int all = sl.last;
+  (void)hipMemsetAsync(sl.acc.data_ptr<int>(), 0, sizeof(int), (hipStream_t)st);
+  *sl.host = 0;
+  return all;
 }
 
 // ba.cpp:32-45 -> cuda_ba (ba_cuda.cu:433-582).  Mutates poses / patches.
@@ -44,6 +160,7 @@ static torch::Tensor ba_forward_ws(torch::Tensor poses, torch::Tensor patches,
   if (E == 0 || iterations <= 0) return torch::Tensor();
   TORCH_CHECK(t1 - t0 <= dpvo_ba_max_free_poses(), "cuda_ba.forward: t1 - t0 = ", t1 - t0,
               " free poses exceeds this build's limit (", dpvo_ba_max_free_poses(), ")");
+  poll_status(poses);  // a previous call's fatal status raises here
   const size_t wsb = dpvo_ba_workspace_bytes(E, t0, t1);
   auto ws = torch::empty({(int64_t)wsb}, poses.options().dtype(torch::kUInt8));
   check_status(dpvo_ba_forward(poses.data_ptr<float>(), patches.data_ptr<float>(),
@@ -54,6 +171,7 @@ static torch::Tensor ba_forward_ws(torch::Tensor poses, torch::Tensor patches,
                                iterations, eff_impl ? 1 : 0, ws.data_ptr(), wsb,
                                current_stream()),
                "cuda_ba.forward");
+  track_status(ws, poses, E, t0, t1);
   return ws;
 }
 
@@ -349,6 +467,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("solve_update", &ba_solve_update, "Cholesky solve + pose/patch retraction");
   m.def("last_status", &ba_last_status, "status word of the last BA on a workspace");
   m.def("max_free_poses", &dpvo_ba_max_free_poses);
+  m.def("check_status", &ba_check_status,
+        "sync on the BA status of every forward so far on the device of `like`; raises "
+        "RuntimeError on fatal bits (2 bad kk, 4/8 large-graph limits, 16 timeout); returns "
+        "the OR of all bits (1 = a Cholesky failure gave a zero step) and resets it");
   m.def("gba_setup", &gba_setup, "large-graph BA setup (ownership own_lo <= kk/PPF < own_hi)");
   m.def("gba_build", &gba_build, "large-graph BA: linearise owned patches -> packed (y, S)");
   m.def("gba_packed", &gba_packed, "view of the packed fp64 [y | S blocks] system");

@@ -148,6 +148,53 @@ def make_graph(F, M, E, seed=0, H=120, W=160, p=3, span=5, noise=0.5, lateral=0.
     return Graph(poses, P, intrinsics, ii, jj, kk, target, weight, F, M)
 
 
+def make_dpvo_window(n=22, M=96, lifetime=13, seed=0, H=120, W=160, p=3, noise=0.5,
+                     intr=(80.0, 80.0, 80.0, 60.0)) -> Graph:
+    """A local-BA window with DPVO's own edge pattern (dpvo/dpvo.py:838-903):
+    when frame f is added its M patches get edges to frames
+    [max(f - lifetime + 1, 0), f] (__edges_back) and every patch of frames
+    [f - lifetime + 1, f) gets an edge to frame f (__edges_forw), so a patch
+    of frame g ends up with edges to frames g-lifetime+1 .. g+lifetime-1
+    inside [0, n).  Edges are in creation order (not grouped by patch), as
+    DPVO's PatchGraph appends them.  E = 394 M for the defaults (n=22,
+    lifetime=13): M = 10 / 18 / 25 -> ~4k / 7k / 10k edges.  Use with
+    t0 = n - OPTIMIZATION_WINDOW (10), t1 = n (dpvo.py:818-824)."""
+    g = torch.Generator().manual_seed(seed)
+    xi = torch.zeros(n, 6, dtype=torch.float64)
+    xi[:, 2] = 0.05 * torch.arange(n, dtype=torch.float64)
+    xi += 0.01 * torch.randn(n, 6, generator=g, dtype=torch.float64)
+    xi[0] = 0
+    poses_np = se3_exp(xi.numpy())
+    cxy = torch.stack([torch.rand(n * M, generator=g) * (W - 9) + 4,
+                       torch.rand(n * M, generator=g) * (H - 9) + 4], -1).floor()
+    d = torch.rand(n * M, generator=g) * 0.8 + 0.3
+    off = torch.arange(p, dtype=torch.float32) - p // 2
+    patches = torch.zeros(n * M, 3, p, p)
+    patches[:, 0] = cxy[:, 0].view(-1, 1, 1) + off.view(1, 1, p)
+    patches[:, 1] = cxy[:, 1].view(-1, 1, 1) + off.view(1, p, 1)
+    patches[:, 2] = d.view(-1, 1, 1)
+    kk, jj = [], []
+    for f in range(n):  # frame f added: forward edges, then backward edges
+        lo = max(f - lifetime + 1, 0)
+        if f > 0:
+            k = torch.arange(lo * M, f * M)
+            kk.append(k)
+            jj.append(torch.full_like(k, f))
+        k = torch.arange(f * M, (f + 1) * M).repeat_interleave(f + 1 - lo)
+        kk.append(k)
+        jj.append(torch.arange(lo, f + 1).repeat(M))
+    kk = torch.cat(kk).long()
+    jj = torch.cat(jj).long()
+    ii = kk // M
+    poses = torch.from_numpy(poses_np).float()
+    intrinsics = torch.tensor(intr).view(1, 4).repeat(n, 1)
+    ctr = reproject_centres(poses.double().numpy(), patches.double().numpy(), intr, ii.numpy(),
+                            jj.numpy(), kk.numpy())
+    target = torch.from_numpy(ctr).float() + noise * torch.randn(len(ii), 2, generator=g)
+    weight = torch.rand(len(ii), 2, generator=g)
+    return Graph(poses, patches, intrinsics, ii, jj, kk, target, weight, n, M)
+
+
 LARGE_CONFIGS = {
     # BASELINE cfg4: 1024 frames x 96 patches, ~131k edges (SURVEY 8d)
     "cfg4": dict(F=1024, M=96, n_random=32000, n_loops=10),

@@ -196,6 +196,16 @@ int dpvo_ba_solve_update(float* poses, float* patches, const double* S_lower, co
    `out`: bit 0 = Cholesky failed in the last solve (dX was set to 0),
    bit 1 = some kk outside [0, num_patches) (clamped). */
 int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1, int* out, void* stream);
+/* OR the status word of the last dpvo_ba_forward on this workspace (any
+   path: window kernels or the large-graph solver) into the DEVICE int `acc`
+   (sticky; the caller resets it).  Bits: 1 Cholesky failed (dX = 0, as
+   dpvo/ba.py:17-21), 2 kk outside [0, num_patches) (clamped), 4 a patch
+   touches more free poses than the large-graph solver handles, 8 too many
+   border poses (large graph), 16 a cross-workgroup wait timed out.  Bits
+   2..16 mean the step was not the reference's and the extension raises.
+   Graph-capturable (one tiny kernel, no host sync). */
+int dpvo_ba_status_accumulate(const void* workspace, int E, int t0, int t1, int* acc,
+                              void* stream);
 /* Instrumentation (no reference counterpart): the 128 marks the last
    dpvo_ba_forward on this workspace stamped -- wall clock (100 MHz): [0]
    start, [1] setup, then linearize, patch, schur, solve, update per iteration;

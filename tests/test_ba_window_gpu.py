@@ -1,0 +1,101 @@
+"""F-BA on DPVO-realistic local-BA windows and BA status surfacing.
+
+Windows: synthetic.make_dpvo_window builds DPVO's own edge pattern
+(dpvo/dpvo.py:838-903: __edges_forw / __edges_back, creation order) over 22
+frames with PATCH_LIFETIME 13; M = 10 / 18 / 25 patches per frame give
+E = 3940 / 7092 / 9850 edges (MAX_EDGES = 10000, dpvo/config.py:42).  The BA
+runs as DPVO's local call does: t0 = n - OPTIMIZATION_WINDOW (10), t1 = n
+(dpvo.py:818-824), so edges into the 12 fixed poses take part.
+Tolerances as tests/test_ba_gpu.py (poses 2e-5 abs, inverse depths 1e-4 rel)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from dpvo_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cb(gpu):
+    import dpvo_amd
+
+    m = dpvo_amd.load_extension("cuda_ba")
+    m.check_status(torch.zeros(1, device=gpu))  # clean slate
+    return m
+
+
+def _run(cb, G, gpu, t0, t1, iters, lm=1e-4):
+    D = G.to(gpu)
+    poses, patches = D.poses.clone(), D.patches.clone()
+    cb.forward(poses, patches, D.intrinsics, D.target, D.weight, torch.tensor([lm], device=gpu),
+               D.ii, D.jj, D.kk, G.M, t0, t1, iters, False)
+    return poses, patches
+
+
+@pytest.mark.parametrize("M", [10, 18, 25])
+@pytest.mark.parametrize("iters", [1, 2])
+def test_dpvo_window_matches_oracle(cb, gpu, M, iters):
+    G = synthetic.make_dpvo_window(M=M, seed=M)
+    n = G.F
+    t0, t1 = n - 10, n
+    P, K = _run(cb, G, gpu, t0, t1, iters)
+    assert cb.check_status(P) == 0
+    Pr, Kr = oracle.ba(G.poses.numpy(), G.patches.numpy(), G.intrinsics.numpy(), G.target.numpy(),
+                       G.weight.numpy(), 1e-4, G.ii.numpy(), G.jj.numpy(), G.kk.numpy(), t0, t1,
+                       iters)
+    P, K = P.cpu().numpy(), K.cpu().numpy()
+    np.testing.assert_allclose(P, Pr, rtol=0, atol=2e-5)
+    np.testing.assert_allclose(K[:, 2], Kr[:, 2], rtol=1e-4, atol=1e-5)
+    np.testing.assert_array_equal(P[:t0], G.poses.numpy()[:t0])  # fixed poses untouched
+    # the window moved: the step is not trivially zero
+    assert np.abs(P[t0:] - G.poses.numpy()[t0:]).max() > 1e-5
+
+
+def test_bad_patch_index_raises(cb, gpu):
+    G = synthetic.make_config("cfg1", seed=3)
+    G.kk = G.kk.clone()
+    G.kk[5] = G.patches.shape[0] + 7  # outside [0, num_patches): clamped on the device
+    _run(cb, G, gpu, 1, G.F, 1)
+    with pytest.raises(RuntimeError, match="status"):
+        cb.check_status(G.poses.to(gpu))
+    # the accumulator was reset by the raise: a clean call reports 0
+    _run(cb, synthetic.make_config("cfg1", seed=4), gpu, 1, 8, 1)
+    assert cb.check_status(G.poses.to(gpu)) == 0
+
+
+def test_deferred_status_raises_on_next_forward(cb, gpu):
+    G = synthetic.make_config("cfg1", seed=5)
+    bad = synthetic.make_config("cfg1", seed=5)
+    bad.kk = bad.kk.clone()
+    bad.kk[0] = -3
+    _run(cb, bad, gpu, 1, bad.F, 1)
+    torch.cuda.synchronize()  # the status copy has landed
+    with pytest.raises(RuntimeError, match="kk outside"):
+        _run(cb, G, gpu, 1, G.F, 1)
+    assert cb.check_status(G.poses.to(gpu)) == 0
+
+
+def test_failed_factorisation_is_reported_not_raised(cb, gpu):
+    G = synthetic.make_config("cfg1", seed=6)
+    G.weight[:] = float("nan")
+    P, _ = _run(cb, G, gpu, 1, G.F, 1)
+    assert cb.check_status(P) & 1
+    assert torch.equal(P.cpu(), G.poses)  # zero step (dpvo/ba.py:17-21)
+
+
+def test_large_graph_structure_limit_raises(cb, gpu):
+    # global BA (N > 16 free poses -> large-graph solver): one patch observed
+    # from 40 free frames exceeds the per-patch free-pose set it handles
+    G = synthetic.make_config("cfg4s", seed=1)
+    k0 = int(G.kk[0])
+    extra_j = torch.arange(2, 42)
+    G.kk = torch.cat([G.kk, torch.full_like(extra_j, k0)])
+    G.ii = G.kk // G.M
+    G.jj = torch.cat([G.jj, extra_j])
+    G.target = torch.cat([G.target, G.target[:1].repeat(len(extra_j), 1)])
+    G.weight = torch.cat([G.weight, G.weight[:1].repeat(len(extra_j), 1)])
+    _run(cb, G, gpu, 1, G.F, 1)
+    with pytest.raises(RuntimeError, match="status"):
+        cb.check_status(G.poses.to(gpu))
