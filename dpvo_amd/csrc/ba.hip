@@ -1076,6 +1076,13 @@ int ba_blocks_launch(float* poses, float* patches, const float* intrinsics, cons
                      const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                      const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
                      int iterations, char* scratch, int* meta, int64_t* marks, void* stream);
+// ba_window.hip: plan kernel + persistent per-block workgroups, solve in every workgroup
+size_t ba_window_scratch_bytes(int E, int N);
+bool ba_window_supported(int E, int N, int P);
+int ba_window_launch(float* poses, float* patches, const float* intrinsics, const float* target,
+                     const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
+                     const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
+                     int iterations, char* scratch, int* status, int64_t* marks, void* stream);
 // ba_large.hip: large graphs (global BA, cfg4)
 size_t gba_workspace_bytes(int E, int N);
 int gba_forward(float* poses, float* patches, const float* intrinsics, const float* target,
@@ -1086,7 +1093,8 @@ int gba_forward(float* poses, float* patches, const float* intrinsics, const flo
 }  // namespace dpvo
 
 namespace {
-// 0 auto (blocks), 1 fused single workgroup, 2 multi-kernel, 3 blocks, 4 large-graph path
+// 0 auto (window), 1 fused single workgroup, 2 multi-kernel, 3 blocks, 4 large-graph path,
+// 5 window
 int g_ba_path = 0;
 }
 
@@ -1147,8 +1155,13 @@ DPVO_EXPORT size_t dpvo_ba_workspace_bytes(int E, int t0, int t1) {
   const int Ep = E > 0 ? E : 1;
   size_t bytes = 0;
   if (window_path_ok(Ep, N)) {
-    const size_t a = ba_fused_scratch_bytes(Ep, N), b = ba_blocks_scratch_bytes(Ep, N);
-    bytes = ba_layout(Ep, N, nullptr, nullptr) + (a > b ? a : b);
+    size_t a = ba_fused_scratch_bytes(Ep, N), b = ba_blocks_scratch_bytes(Ep, N);
+    a = a > b ? a : b;
+    if (ba_window_supported(Ep, N, 3)) {
+      const size_t c = ba_window_scratch_bytes(Ep, N);
+      a = a > c ? a : c;
+    }
+    bytes = ba_layout(Ep, N, nullptr, nullptr) + a;
   }
   if (use_large(Ep, N)) {
     const size_t g = gba_workspace_bytes(Ep, N);
@@ -1158,7 +1171,7 @@ DPVO_EXPORT size_t dpvo_ba_workspace_bytes(int E, int t0, int t1) {
 }
 
 DPVO_EXPORT int dpvo_ba_select_path(int mode) {
-  if (mode < 0 || mode > 4) return DPVO_ERR_INVALID;
+  if (mode < 0 || mode > 5) return DPVO_ERR_INVALID;
   g_ba_path = mode;
   return DPVO_OK;
 }
@@ -1315,7 +1328,11 @@ DPVO_EXPORT int dpvo_ba_forward(float* poses, float* patches, const float* intri
                        workspace_bytes, stream);
   BaWs w;
   const size_t base_bytes = ba_layout(E, N, (char*)workspace, &w);
-  if ((g_ba_path == 0 || g_ba_path == 3) && ba_blocks_supported(E, N, P))
+  if ((g_ba_path == 0 || g_ba_path == 5) && ba_window_supported(E, N, P))
+    return ba_window_launch(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
+                            num_poses, num_patches, t0, t1, iterations,
+                            (char*)workspace + base_bytes, w.meta + 1, w.tmark, stream);
+  if (g_ba_path == 3 && ba_blocks_supported(E, N, P))
     return ba_blocks_launch(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
                             num_poses, num_patches, t0, t1, iterations,
                             (char*)workspace + base_bytes, w.meta, w.tmark, stream);

@@ -1,0 +1,982 @@
+// ba_window.hip -- F-BA for DPVO local-BA windows (N <= 16 free poses,
+// E <= 4096 edges): the default path of cuda_ba.forward for those shapes.
+//
+// Reference semantics: dpvo/fastba/ba_cuda.cu:433-582 (block_e.cu:188-300 for
+// the block-sparse E):
+//   per edge: residual + Jacobians in fp32 (ba_cuda.cu:265-333)
+//   B, E, C, v, u (:339-373); Q = 1/(C + lmbda) (:519)
+//   S = B - E Q E^T, y = v - E Q u (:554-558), S += I (1e-4 S + 1) (:560)
+//   dX = chol_solve(S, y) (:561-562), dZ = Q (u - E^T dX) (:563)
+//   pose_retr_kernel (:178-206), patch_retr_kernel (:209-229).
+//
+// MI355X design (DESIGN.md "F-BA for DPVO windows").  A window is
+// latency-bound (~0.5 MB of compulsory traffic per call), so the aim is the
+// shortest dependency chain, not bandwidth:
+//   * ba_plan_kernel (one 1024-thread workgroup, depends on ii/jj/kk only):
+//     groups the edges by patch ONCE (counting sort on kk in LDS, bitonic if
+//     the kk range is too wide; deterministic order inside a patch) and
+//     writes patch offsets + free-pose masks.  Because it reads no pose,
+//     target or weight it can run concurrently with A-CORR.
+//   * ba_window_kernel: persistent, one workgroup per (lower 6x6 block (a, b)
+//     of S, share `sub` of its patches).  Each workgroup keeps the patches
+//     whose free-pose mask holds both a and b, re-linearises their edges each
+//     iteration (fp32 edge math, fp64 products), reduces its block in a fixed
+//     order (no atomics: deterministic) and publishes 42 doubles.  EVERY
+//     workgroup then gathers all partial blocks (fixed order -> identical
+//     bits everywhere), solves S dX = y itself (ba_solve.hpp, fp32 blocked
+//     Cholesky + fp64 refinement) and applies the same pose retraction and
+//     the depth update of its own patches.  One grid-wide exchange per
+//     iteration; no solve -> broadcast hand-off.
+//   * Grid <= 256 workgroups (one per CU, all co-resident); flags are
+//     epoch-tagged (graph-replayable) and every spin-wait has a wall-clock
+//     timeout (status bit 16) so the grid always drains.
+#include <map>
+#include <mutex>
+
+#include "ba_solve.hpp"
+
+namespace dpvo {
+namespace {
+using namespace bad;
+
+constexpr int kWT = 256;                // iteration kernel threads
+constexpr int kPT = 1024;               // plan kernel threads
+constexpr int kWMaxN = 16;
+constexpr int kWMaxE = 4096;
+constexpr int kWMaxG = 256;
+constexpr int kWLds = 160 * 1024;
+constexpr int kHistMax = 12288;         // counting-sort range of kk
+constexpr int kWSlots = 64;             // LDS pose table slots
+constexpr unsigned kFix = 0xFF;         // pose code: fixed pose
+constexpr unsigned kHbm = 0xFE;         // pose slot: read from HBM
+constexpr int kChunk = 256;             // relevant edges per pass-1 chunk
+constexpr int kPart = 42;               // doubles per published partial block
+constexpr long long kSpin = 2000000;    // 20 ms of the 100 MHz wall clock
+constexpr int kEpochWord = kWMaxG;      // flags[kWMaxG]: epoch of the last call
+constexpr int kFlagWords = kWMaxG + 8;
+constexpr int kRefine = 1;              // fp64 refinement steps of the solve
+
+// status bits (shared with the other BA paths; see dpvo_hot.h)
+constexpr int kStChol = 1, kStClamp = 2, kStTimeout = 16, kStCap = 32;
+
+struct Plan {          // written by ba_plan_kernel, read by ba_window_kernel
+  int* epos;           // [E] edge index at sorted position p (grouped by patch)
+  int* poff;           // [E + 1] first position of patch u
+  unsigned* pmask;     // [E] free-pose bitmask of patch u
+  int* pkk;            // [E] patch id (kk) of patch u
+  int* meta;           // [8] nuniq, fmin, status
+};
+
+struct WArgs {
+  float* poses;
+  float* patches;
+  const float* intrinsics;
+  const float* target;
+  const float* weight;
+  const float* lmbda;
+  const int64_t* ii;
+  const int64_t* jj;
+  const int64_t* kk;
+  int E, P, num_poses, num_patches, t0, N, iters, NB, Sd, So, G;
+  Plan plan;
+  double* part;      // [G][kPart] published partial blocks
+  long long* flags;  // persistent [kFlagWords]
+  float* ejg;        // [G][E][12] per relevant edge E entries (fp32), HBM fallback
+  int* status;       // [1] OR of status bits (workspace meta)
+  int64_t* marks;    // [64] wall-clock stamps of workgroup 0 (may be null)
+};
+
+__device__ __forceinline__ size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
+
+__device__ bool wait_flag(long long* p, long long target) {
+  const long long t0 = (long long)wall_clock64();
+  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if ((long long)wall_clock64() - t0 > kSpin) return false;
+  }
+  return true;
+}
+
+__device__ __forceinline__ void mark(const WArgs& A, int slot) {
+  if (A.marks && blockIdx.x == 0 && threadIdx.x == 0) A.marks[slot] = (int64_t)wall_clock64();
+}
+
+// workgroup g -> (block a, b; share sub of S shares).  Diagonal blocks first.
+__device__ __forceinline__ void wg_block(const WArgs& A, int g, int& a, int& b, int& sub, int& S) {
+  const int nd = A.N * A.Sd;
+  if (g < nd) {
+    a = b = g / A.Sd;
+    sub = g % A.Sd;
+    S = A.Sd;
+  } else {
+    const int o = (g - nd) / A.So;  // o-th strictly lower block, row-major
+    sub = (g - nd) % A.So;
+    S = A.So;
+    a = 1;  // (a, b), a > b, at o = a(a-1)/2 + b
+    while ((a + 1) * a / 2 <= o) a++;
+    b = o - a * (a - 1) / 2;
+  }
+}
+
+// ===========================================================================
+// plan: group edges by patch (one workgroup, 1024 threads)
+// ===========================================================================
+__global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict__ ii,
+                                                      const int64_t* __restrict__ jj,
+                                                      const int64_t* __restrict__ kk, int E,
+                                                      int num_patches, int num_poses, int t0, int N,
+                                                      Plan plan) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, T = kPT;
+  int* ctl = (int*)lds;                  // [64]
+  int* scr = ctl + 16;                   // scan scratch [>= 17]
+  unsigned* code = (unsigned*)(lds + 256);                        // [E] ci | cj << 8
+  char* big = lds + 256 + al16(sizeof(unsigned) * kWMaxE);       // sort area
+  const int kmaxc = num_patches - 1;
+  if (tid == 0) {
+    ctl[0] = 0x7fffffff;  // kmin
+    ctl[1] = -1;          // kmax
+    ctl[2] = 0x7fffffff;  // fmin
+    ctl[3] = 0;           // status
+  }
+  __syncthreads();
+  int kmin = 0x7fffffff, kmax = -1, fmin = 0x7fffffff, bad = 0;
+  for (int e = tid; e < E; e += T) {
+    int64_t v = kk[e];
+    if (v < 0 || v > kmaxc) {
+      bad = 1;
+      v = v < 0 ? 0 : kmaxc;
+    }
+    kmin = min(kmin, (int)v);
+    kmax = max(kmax, (int)v);
+    const int64_t gi = ii[e], gj = jj[e];
+    const bool fi = gi >= t0 && gi < t0 + N, fj = gj >= t0 && gj < t0 + N;
+    const int ci = fi ? (int)(gi - t0) : (int)kFix, cj = fj ? (int)(gj - t0) : (int)kFix;
+    if (!fi) fmin = min(fmin, (int)min(max(gi, (int64_t)0), (int64_t)num_poses - 1));
+    if (!fj) fmin = min(fmin, (int)min(max(gj, (int64_t)0), (int64_t)num_poses - 1));
+    code[e] = (unsigned)ci | ((unsigned)cj << 8);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    kmin = min(kmin, __shfl_xor(kmin, o, 64));
+    kmax = max(kmax, __shfl_xor(kmax, o, 64));
+    fmin = min(fmin, __shfl_xor(fmin, o, 64));
+    bad |= __shfl_xor(bad, o, 64);
+  }
+  if (lane == 0) {
+    atomicMin(&ctl[0], kmin);
+    atomicMax(&ctl[1], kmax);
+    atomicMin(&ctl[2], fmin);
+    if (bad) atomicOr(&ctl[3], kStClamp);
+  }
+  __syncthreads();
+  kmin = ctl[0];
+  const int R = ctl[1] - kmin + 1;
+  int* spos = (int*)big;                 // [E] edge at position p
+  int* head = spos + kWMaxE;             // [E] head flags -> patch index (scan)
+  auto key_of = [&](int e) -> int {
+    int64_t v = kk[e];
+    v = v < 0 ? 0 : (v > kmaxc ? kmaxc : v);
+    return (int)v - kmin;
+  };
+  if (R <= kHistMax) {
+    int* hist = head + kWMaxE;           // [R]
+    for (int v = tid; v < R; v += T) hist[v] = 0;
+    __syncthreads();
+    for (int e = tid; e < E; e += T) atomicAdd(&hist[key_of(e)], 1);
+    __syncthreads();
+    fscan(hist, R, scr);                 // hist[v] = first position of bucket v
+    for (int p = tid; p < E; p += T) head[p] = 0;
+    __syncthreads();
+    for (int v = tid; v < R; v += T) {
+      const int a = hist[v], b = (v + 1 < R) ? hist[v + 1] : E;
+      if (b > a) head[a] = 1;
+    }
+    for (int e = tid; e < E; e += T) spos[atomicAdd(&hist[key_of(e)], 1)] = e;
+    __syncthreads();
+    // deterministic order inside a patch: ascending edge index (buckets are tiny)
+    for (int v = tid; v < R; v += T) {
+      const int b = hist[v], a = (v == 0) ? 0 : hist[v - 1];
+      for (int t = a + 1; t < b; t++) {
+        const int x = spos[t];
+        int s2 = t - 1;
+        while (s2 >= a && spos[s2] > x) {
+          spos[s2 + 1] = spos[s2];
+          s2--;
+        }
+        spos[s2 + 1] = x;
+      }
+    }
+  } else {
+    // wide kk range: bitonic sort of (key << 32 | e) over the next power of two
+    int P2 = 1;
+    while (P2 < E) P2 <<= 1;
+    unsigned long long* keys = (unsigned long long*)(head + kWMaxE);
+    for (int i = tid; i < P2; i += T)
+      keys[i] = (i < E) ? (((unsigned long long)(unsigned)key_of(i) << 32) | (unsigned)i) : ~0ull;
+    __syncthreads();
+    for (int size = 2; size <= P2; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = tid; i < P2 / 2; i += T) {
+          const int lo = 2 * i - (i & (stride - 1));
+          const int hi = lo + stride;
+          const bool up = ((lo & size) == 0);
+          const unsigned long long a = keys[lo], b = keys[hi];
+          if ((a > b) == up) {
+            keys[lo] = b;
+            keys[hi] = a;
+          }
+        }
+        __syncthreads();
+      }
+    for (int p = tid; p < E; p += T) {
+      spos[p] = (int)(keys[p] & 0xffffffffull);
+      head[p] = (p == 0 || (keys[p] >> 32) != (keys[p - 1] >> 32)) ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  // patch index of every position: inclusive scan of the heads
+  int* hd = head;
+  const int nuniq = fscan(hd, E, scr);   // hd[p] = heads strictly before p
+  // patch u starts at the p with hd[p] == u and a head: recompute heads
+  for (int p = tid; p < E; p += T) {
+    const int u1 = (p + 1 < E) ? hd[p + 1] : nuniq;  // heads up to and including p
+    const bool is_head = u1 != hd[p];
+    const int u = u1 - 1;                            // patch of position p
+    const int e = spos[p];
+    plan.epos[p] = e;
+    if (is_head) {
+      plan.poff[u] = p;
+      plan.pkk[u] = key_of(e) + kmin;
+    }
+  }
+  if (tid == 0) plan.poff[nuniq] = E;
+  // free-pose masks: OR over the patch's edges (positions are contiguous)
+  unsigned* mask = (unsigned*)(hd + kWMaxE);  // [nuniq] (past the sort keys' first half)
+  __syncthreads();
+  for (int u = tid; u < nuniq; u += T) mask[u] = 0u;
+  __syncthreads();
+  for (int p = tid; p < E; p += T) {
+    const int u = ((p + 1 < E) ? hd[p + 1] : nuniq) - 1;
+    const unsigned c = code[spos[p]];
+    const unsigned ci = c & 0xff, cj = c >> 8;
+    const unsigned m = (ci != kFix ? 1u << ci : 0u) | (cj != kFix ? 1u << cj : 0u);
+    if (m) atomicOr(&mask[u], m);
+  }
+  __syncthreads();
+  for (int u = tid; u < nuniq; u += T) plan.pmask[u] = mask[u];
+  if (tid == 0) {
+    plan.meta[0] = nuniq;
+    plan.meta[1] = ctl[2];
+    plan.meta[2] = ctl[3];
+  }
+}
+
+// ===========================================================================
+// iteration kernel
+// ===========================================================================
+struct WL {  // LDS layout of one workgroup
+  int* ctl;            // [64]
+  float* pose;         // [kWSlots][8]
+  double* dX;          // [6N]
+  unsigned short* tri;  // [NB] block (a, b) of lower-block index (a << 8 | b)
+  // relevant patches
+  int* roff;           // [nrel + 1] first relevant edge
+  float2* nxy;         // [nrel] normalised centre
+  float* dep;          // [nrel] inverse depth (current)
+  float* dbase;        // [nrel] [2][0][0] of the input (first retraction base)
+  double2* qu;         // [nrel] Q, u of the last linearisation
+  int* pkx;            // [nrel] patch id, -1 if this workgroup does not write it
+  // relevant edges
+  unsigned short* ec;  // [nrp] pose slot of ii | slot of jj << 8
+  unsigned short* rp;  // [nrp] relevant patch of the edge
+  int* eid;            // [nrp] edge index
+  float4* tw;          // [nrp] target, weight (LDS or HBM)
+  float* ej;           // [nrp][12] E entries of the last linearisation (LDS or HBM)
+  char* region;        // union: chunk scratch / reduction table / solver
+};
+
+enum { cNrel = 0, cNrp = 1, cFmin = 2, cFail = 3, cTimeout = 4, cCap = 5, cScan = 16 };
+
+__device__ __forceinline__ unsigned wslot(int gp, int t0, int N, int fmin) {
+  if (gp >= t0 && gp < t0 + N) return (unsigned)(gp - t0);
+  const int k = gp - fmin;
+  return (k >= 0 && k < kWSlots - N) ? (unsigned)(N + k) : kHbm;
+}
+
+__device__ __forceinline__ void pose_of(const WArgs& A, const WL& L, unsigned slot, int gp,
+                                        float* P) {
+  if (slot != kHbm) {
+    const float4 a0 = *reinterpret_cast<const float4*>(L.pose + 8 * slot);
+    const float4 a1 = *reinterpret_cast<const float4*>(L.pose + 8 * slot + 4);
+    P[0] = a0.x; P[1] = a0.y; P[2] = a0.z; P[3] = a0.w; P[4] = a1.x; P[5] = a1.y; P[6] = a1.z;
+  } else {
+    const float* g = A.poses + 7 * (size_t)gp;
+#pragma unroll
+    for (int k = 0; k < 7; k++) P[k] = g[k];
+  }
+}
+
+template <int MODE>  // 0: only Q, u (no free pose / N == 0); 1 diagonal block; 2 off-diagonal
+__device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, double lam,
+                         float fx, float fy, float cx, float cy, double* acc) {
+  constexpr int NA = (MODE == 1) ? 27 : (MODE == 2 ? 36 : 1);
+  const int tid = threadIdx.x, N = A.N;
+  const unsigned ua = (unsigned)a, ub = (unsigned)b;
+  double* pe = reinterpret_cast<double*>(L.region);  // [kChunk][14]: c, u, Ea[6], Eb[6]
+#pragma unroll
+  for (int k = 0; k < NA; k++) acc[k] = 0.0;
+  for (int pa = 0; pa < nrel;) {
+    // chunk: whole patches [pa, pb) with at most kChunk edges (one patch may exceed: own chunk)
+    int pb = pa + 1;
+    {
+      int lo = pa + 1, hi = nrel;  // largest pb with roff[pb] - roff[pa] <= kChunk
+      const int base = L.roff[pa];
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (L.roff[mid] - base <= kChunk) lo = mid; else hi = mid - 1;
+      }
+      pb = lo;
+    }
+    const int q0 = L.roff[pa], q1 = L.roff[pb];
+    // pass 1: thread per edge
+    for (int q = q0 + tid; q < q1; q += kWT) {
+      const unsigned c = L.ec[q];
+      const unsigned si = c & 0xff, sj = c >> 8;
+      const int e = L.eid[q];
+      float Pi[7], Pj[7];
+      pose_of(A, L, si, si == kHbm ? (int)A.ii[e] : 0, Pi);
+      pose_of(A, L, sj, sj == kHbm ? (int)A.jj[e] : 0, Pj);
+      const int ri = L.rp[q];
+      const float4 tw = L.tw[q];
+      Lin o;
+      lin_edge(Pi, Pj, L.nxy[ri].x, L.nxy[ri].y, L.dep[ri], tw.x, tw.y, tw.z, tw.w, fx, fy, cx,
+               cy, o);
+      const unsigned ci = si < (unsigned)N ? si : kFix, cj = sj < (unsigned)N ? sj : kFix;
+      double cq = 0.0, uq = 0.0, ejv[6] = {0, 0, 0, 0, 0, 0}, eiv[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int row = 0; row < 2; row++) {
+        const double wr = o.w[row];
+        const double wz = wr * (double)o.Jz[row];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+          ejv[k] += wz * (double)o.Jj[row][k];
+          eiv[k] -= wz * (double)o.Ji[row][k];
+        }
+        cq += wz * (double)o.Jz[row];
+        uq += (wr * (double)o.r[row]) * (double)o.Jz[row];
+      }
+      // E entries (fp32) for the depth update after the solve
+      float4* eo = reinterpret_cast<float4*>(L.ej + 12 * (size_t)q);
+      eo[0] = make_float4((float)ejv[0], (float)ejv[1], (float)ejv[2], (float)ejv[3]);
+      eo[1] = make_float4((float)ejv[4], (float)ejv[5], (float)eiv[0], (float)eiv[1]);
+      eo[2] = make_float4((float)eiv[2], (float)eiv[3], (float)eiv[4], (float)eiv[5]);
+      double* ps = pe + 14 * (size_t)(q - q0);
+      ps[0] = cq;
+      ps[1] = uq;
+      if (MODE != 0) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+          ps[2 + k] = ((cj == ua) ? ejv[k] : 0.0) + ((ci == ua) ? eiv[k] : 0.0);
+          ps[8 + k] = ((cj == ub) ? ejv[k] : 0.0) + ((ci == ub) ? eiv[k] : 0.0);
+        }
+        // B terms of this block (ba_cuda.cu:339-350), v (:352-370)
+        const bool ia = ci == ua, ja = cj == ua, ib = ci == ub, jb = cj == ub;
+        const bool hit = (MODE == 1) ? (ia || ja) : ((ia && jb) || (ja && ib));
+        if (hit) {
+#pragma unroll
+          for (int row = 0; row < 2; row++) {
+            double Rv[6], Cv[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+              const double ji = o.Ji[row][k], jv = o.Jj[row][k];
+              if (MODE == 1) {
+                Rv[k] = (ia ? ji : 0.0) - (ja ? jv : 0.0);
+                Cv[k] = Rv[k];
+              } else {
+                Rv[k] = ia ? ji : jv;
+                Cv[k] = ia ? jv : ji;
+              }
+            }
+            const double wr = o.w[row];
+            const double coef = (MODE == 1) ? wr : -wr;
+            int k = 0;
+#pragma unroll
+            for (int x = 0; x < 6; x++) {
+              const double t = coef * Rv[x];
+              if (MODE == 1) {
+#pragma unroll
+                for (int z = 0; z <= x; z++) acc[k++] += t * Cv[z];
+              } else {
+#pragma unroll
+                for (int z = 0; z < 6; z++) acc[6 * x + z] += t * Cv[z];
+              }
+            }
+            if (MODE == 1) {
+              const double wrr = wr * (double)o.r[row];
+#pragma unroll
+              for (int x = 0; x < 6; x++) acc[21 + x] -= wrr * Rv[x];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // pass 2: thread per patch: C, u, E at a / b in edge order; Schur terms (:554-558)
+    for (int ri = pa + tid; ri < pb; ri += kWT) {
+      double C = 0.0, U = 0.0, Ea[6] = {0, 0, 0, 0, 0, 0}, Eb[6] = {0, 0, 0, 0, 0, 0};
+      for (int q = L.roff[ri]; q < L.roff[ri + 1]; q++) {
+        const double* ps = pe + 14 * (size_t)(q - q0);
+        C += ps[0];
+        U += ps[1];
+        if (MODE != 0) {
+#pragma unroll
+          for (int k = 0; k < 6; k++) {
+            Ea[k] += ps[2 + k];
+            if (MODE == 2) Eb[k] += ps[8 + k];
+          }
+        }
+      }
+      const double Q = 1.0 / (C + lam);  // (:519)
+      L.qu[ri] = make_double2(Q, U);
+      if (MODE == 1) {
+        int k = 0;
+#pragma unroll
+        for (int x = 0; x < 6; x++) {
+          const double qa = Q * Ea[x];
+#pragma unroll
+          for (int z = 0; z <= x; z++) acc[k++] -= qa * Ea[z];
+          acc[21 + x] -= (Q * U) * Ea[x];
+        }
+      } else if (MODE == 2) {
+#pragma unroll
+        for (int x = 0; x < 6; x++) {
+          const double qa = Q * Ea[x];
+#pragma unroll
+          for (int z = 0; z < 6; z++) acc[6 * x + z] -= qa * Eb[z];
+        }
+      }
+    }
+    __syncthreads();
+    pa = pb;
+  }
+}
+
+// fixed-order workgroup reduction of NA accumulators per thread -> out[0..NA)
+template <int NA>
+__device__ void reduce_acc(const double* acc, double* red, double* out) {
+  const int tid = threadIdx.x;
+  // two rounds of 128 columns: red[v][col]
+  if (tid >= 128) {
+#pragma unroll
+    for (int v = 0; v < NA; v++) red[v * 128 + tid - 128] = acc[v];
+  }
+  __syncthreads();
+  if (tid < 128) {
+#pragma unroll
+    for (int v = 0; v < NA; v++) red[v * 128 + tid] += acc[v];
+  }
+  __syncthreads();
+  // 8 segments of 16 columns per value, 4 independent partial sums each
+  double* seg = red + NA * 128;
+  for (int t = tid; t < NA * 8; t += kWT) {
+    const int v = t >> 3, s = t & 7;
+    const double* r = red + v * 128 + 16 * s;
+    double p0 = r[0] + r[1], p1 = r[2] + r[3], p2 = r[4] + r[5], p3 = r[6] + r[7];
+    p0 += r[8] + r[9];
+    p1 += r[10] + r[11];
+    p2 += r[12] + r[13];
+    p3 += r[14] + r[15];
+    seg[t] = (p0 + p1) + (p2 + p3);
+  }
+  __syncthreads();
+  if (tid < NA) {
+    const double* s = seg + 8 * tid;
+    const double v = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+    __hip_atomic_store(out + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, g = blockIdx.x;
+  const int N = A.N, P = A.P, PP = P * P, NB = A.NB;
+  int a = 0, b = 0, sub = 0, S = 1;
+  if (NB > 0) wg_block(A, g, a, b, sub, S);
+  const bool diag = (a == b);
+  const float fx = A.intrinsics[0], fy = A.intrinsics[1], cx = A.intrinsics[2],
+              cy = A.intrinsics[3];
+  // this call's tag: every workgroup reads it at entry; workgroup 0 advances it
+  // at its very end (after everyone has read it: they all arrive in iteration 0)
+  const long long epoch =
+      __hip_atomic_load(&A.flags[kEpochWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  mark(A, 0);
+
+  WL L;
+  L.ctl = (int*)lds;
+  int* ctl = L.ctl;
+  int* scr = ctl + cScan;
+  L.pose = (float*)(lds + 256);
+  L.dX = (double*)(lds + 256 + sizeof(float) * 8 * kWSlots);
+  L.tri = (unsigned short*)(lds + 256 + sizeof(float) * 8 * kWSlots + sizeof(double) * 6 * kWMaxN);
+  size_t off = al16(256 + sizeof(float) * 8 * kWSlots + sizeof(double) * 6 * kWMaxN +
+                    sizeof(unsigned short) * (kWMaxN * (kWMaxN + 1) / 2));
+  for (int t = tid; t < NB; t += kWT) {
+    int ta, tb;
+    tri_of(t, ta, tb);
+    L.tri[t] = (unsigned short)((ta << 8) | tb);
+  }
+  const int nuniq = A.plan.meta[0], fmin = A.plan.meta[1];
+  if (tid == 0) {
+    ctl[cFail] = 0;
+    ctl[cTimeout] = 0;
+    ctl[cCap] = 0;
+  }
+
+  // ---------------- setup: relevant patches of this workgroup ----------------
+  // rel(u): mask holds a and b and u % S == sub; workgroup 0 also takes the
+  // patches without a free pose (their dZ = Q u).  One scan packs
+  // (#patches << 16 | #edges) (E <= 4096 keeps both below 2^16).
+  const unsigned need = (NB > 0) ? ((1u << a) | (1u << b)) : 0u;
+  int* cnt = (int*)(lds + off);  // [nuniq] scan input / prefix (kept until the records are built)
+  for (int u = tid; u < nuniq; u += kWT) {
+    const unsigned m = A.plan.pmask[u];
+    const bool rel = (NB == 0) ? true
+                               : (((m & need) == need && (u % S) == sub) || (g == 0 && m == 0));
+    cnt[u] = rel ? ((1 << 16) | (A.plan.poff[u + 1] - A.plan.poff[u])) : 0;
+  }
+  __syncthreads();
+  const int tot = fscan(cnt, nuniq, scr);
+  int nrel = tot >> 16, nrp = tot & 0xffff;
+  // LDS plan: [head | cnt | patch records | edge records | region | tw | ej]
+  const size_t chunk_b = sizeof(double) * 14 * kChunk;
+  const size_t red_b = sizeof(double) * (36 * 128 + 36 * 8);
+  const size_t NN = N > 0 ? N : 1;
+  const size_t solve_b =
+      sizeof(double) * (36 * (NN * (NN + 1) / 2) + 6 * NN) + wsolve_bytes((int)NN) + 64;
+  // gather: S, y and a copy of every published partial (read with one wave of loads)
+  const size_t gather_b = sizeof(double) * (36 * (NN * (NN + 1) / 2) + 6 * NN + (size_t)kPart * A.G);
+  size_t region_b = chunk_b > red_b ? chunk_b : red_b;
+  region_b = region_b > solve_b ? region_b : solve_b;
+  region_b = region_b > gather_b ? region_b : gather_b;
+  const size_t rec0 = al16(off + sizeof(int) * (nuniq + 1));
+  auto rec_bytes = [&](int nr, int ne) {
+    return al16(sizeof(int) * (nr + 1)) + al16(sizeof(float2) * (nr + 1)) +
+           2 * al16(sizeof(float) * (nr + 1)) + al16(sizeof(double2) * (nr + 1)) +
+           al16(sizeof(int) * (nr + 1)) + 2 * al16(sizeof(unsigned short) * (ne + 1)) +
+           al16(sizeof(int) * (ne + 1));
+  };
+  bool fits = rec0 + rec_bytes(nrel, nrp) + region_b <= (size_t)kWLds;
+  if (!fits) {  // contributes nothing; the call reports status 32 (raised by the extension)
+    if (tid == 0) atomicOr(A.status, kStCap);
+    nrel = nrp = 0;
+  }
+  size_t o2 = rec0;
+  auto take = [&](size_t bytes) {
+    char* p = lds + o2;
+    o2 = al16(o2 + bytes);
+    return p;
+  };
+  L.roff = (int*)take(sizeof(int) * (nrel + 1));
+  L.nxy = (float2*)take(sizeof(float2) * (nrel + 1));
+  L.dep = (float*)take(sizeof(float) * (nrel + 1));
+  L.dbase = (float*)take(sizeof(float) * (nrel + 1));
+  L.qu = (double2*)take(sizeof(double2) * (nrel + 1));
+  L.pkx = (int*)take(sizeof(int) * (nrel + 1));
+  L.ec = (unsigned short*)take(sizeof(unsigned short) * (nrp + 1));
+  L.rp = (unsigned short*)take(sizeof(unsigned short) * (nrp + 1));
+  L.eid = (int*)take(sizeof(int) * (nrp + 1));
+  L.region = take(region_b);
+  // target/weight and E entries in LDS when they fit, else this workgroup's HBM scratch
+  const size_t tw_b = sizeof(float4) * (nrp + 1), ej_b = sizeof(float) * 12 * (nrp + 1);
+  float4* tw_hbm = reinterpret_cast<float4*>(A.ejg + (size_t)g * A.E * 16);
+  float* ej_hbm = A.ejg + (size_t)g * A.E * 16 + 4 * (size_t)A.E;
+  if (o2 + tw_b + ej_b <= (size_t)kWLds) {
+    L.tw = (float4*)take(tw_b);
+    L.ej = (float*)take(ej_b);
+  } else if (o2 + tw_b <= (size_t)kWLds) {
+    L.tw = (float4*)take(tw_b);
+    L.ej = ej_hbm;
+  } else {
+    L.tw = tw_hbm;
+    L.ej = ej_hbm;
+  }
+  // pass A, thread per relevant patch: records, edge offsets, patch of each edge
+  int* rpo = reinterpret_cast<int*>(L.qu);  // first sorted position (until the first linearisation)
+  for (int u = tid; u < nuniq && nrel > 0; u += kWT) {
+    const int c0 = cnt[u], c1 = (u + 1 < nuniq) ? cnt[u + 1] : tot;
+    if (c1 == c0) continue;
+    const int ri = c0 >> 16, q0 = c0 & 0xffff, ne = (c1 - c0) & 0xffff;
+    L.roff[ri] = q0;
+    rpo[ri] = A.plan.poff[u];
+    for (int t = 0; t < ne; t++) L.rp[q0 + t] = (unsigned short)ri;
+    if (ne > kChunk) atomicOr(A.status, kStCap);
+    const int kx = A.plan.pkk[u];
+    const float* pk = A.patches + (size_t)kx * 3 * PP;
+    const int c11 = P + 1;  // [*][1][1] (ba_cuda.cu:282-285)
+    const float px = pk[c11], py = pk[PP + c11];
+    L.nxy[ri] = make_float2((px - cx) / fx, (py - cy) / fy);
+    L.dep[ri] = pk[2 * PP + c11];
+    L.dbase[ri] = pk[2 * PP];  // patch_retr_kernel reads [2][0][0] (:225)
+    // writer of the final depth: the diagonal workgroup of the lowest free
+    // pose with share u % Sd; workgroup 0 for patches without a free pose
+    const unsigned m = A.plan.pmask[u];
+    bool own;
+    if (NB == 0) own = true;
+    else if (m == 0) own = (g == 0);
+    else own = diag && (int)__builtin_ctz(m) == a && (u % A.Sd) == sub;
+    L.pkx[ri] = own ? kx : -1;
+  }
+  if (tid == 0) L.roff[nrel] = nrp;
+  __syncthreads();
+  // pass B, thread per relevant edge: slots, edge index, target/weight
+  for (int q = tid; q < nrp; q += kWT) {
+    const int ri = L.rp[q];
+    const int e = A.plan.epos[rpo[ri] + (q - L.roff[ri])];
+    const unsigned si = wslot((int)A.ii[e], A.t0, N, fmin), sj = wslot((int)A.jj[e], A.t0, N, fmin);
+    L.ec[q] = (unsigned short)(si | (sj << 8));
+    L.eid[q] = e;
+    const float2 tg = reinterpret_cast<const float2*>(A.target)[e];
+    const float2 wt = reinterpret_cast<const float2*>(A.weight)[e];
+    L.tw[q] = make_float4(tg.x, tg.y, wt.x, wt.y);
+  }
+  // pose table: free poses t0.., then fixed ones from fmin
+  for (int k = tid; k < kWSlots * 8; k += kWT) {
+    const int sl = k >> 3, c = k & 7;
+    const int gp = (sl < N) ? A.t0 + sl : fmin + (sl - N);
+    float v = (c == 6) ? 1.0f : 0.0f;
+    if (c < 7 && gp >= 0 && gp < A.num_poses && (sl < N || fmin != 0x7fffffff))
+      v = A.poses[7 * (size_t)gp + c];
+    L.pose[k] = v;
+  }
+  __syncthreads();
+  mark(A, 1);
+  const int nrel_e = nrel;
+
+  // ---------------- iterations ----------------
+  const double lam = (double)A.lmbda[0];
+  for (int it = 0; it < A.iters; it++) {
+    const int mb = 2 + 8 * it;
+    if (it > 0) {
+      // ---- apply dX of iteration it-1: poses, then inverse depths ----
+      for (int i = tid; i < N; i += kWT) {  // pose_retr_kernel (:178-206)
+        float xi[6], tt[3], qq[4], t1[3], q1[4];
+#pragma unroll
+        for (int k = 0; k < 6; k++) xi[k] = (float)L.dX[6 * i + k];
+        float* pl = L.pose + 8 * i;
+        tt[0] = pl[0]; tt[1] = pl[1]; tt[2] = pl[2];
+        qq[0] = pl[3]; qq[1] = pl[4]; qq[2] = pl[5]; qq[3] = pl[6];
+        retrSE3(xi, tt, qq, t1, q1);
+        pl[0] = t1[0]; pl[1] = t1[1]; pl[2] = t1[2];
+        pl[3] = q1[0]; pl[4] = q1[1]; pl[5] = q1[2]; pl[6] = q1[3];
+      }
+      for (int ri = tid; ri < nrel_e; ri += kWT) {  // dZ = Q (u - E^T dX) (:563), patch_retr (:209-229)
+        double ex = 0.0;
+        for (int q = L.roff[ri]; q < L.roff[ri + 1]; q++) {
+          const unsigned c = L.ec[q];
+          const unsigned si = c & 0xff, sj = c >> 8;
+          const float4* e4 = reinterpret_cast<const float4*>(L.ej + 12 * (size_t)q);
+          const float4 e0 = e4[0], e1 = e4[1], e2 = e4[2];
+          if (sj < (unsigned)N) {
+            const double* d = L.dX + 6 * sj;
+            ex += (double)e0.x * d[0] + (double)e0.y * d[1] + (double)e0.z * d[2] +
+                  (double)e0.w * d[3] + (double)e1.x * d[4] + (double)e1.y * d[5];
+          }
+          if (si < (unsigned)N) {
+            const double* d = L.dX + 6 * si;
+            ex += (double)e1.z * d[0] + (double)e1.w * d[1] + (double)e2.x * d[2] +
+                  (double)e2.y * d[3] + (double)e2.z * d[4] + (double)e2.w * d[5];
+          }
+        }
+        const double2 qu = L.qu[ri];
+        const float dz = (float)(qu.x * (qu.y - ex));
+        const float base = (it == 1) ? L.dbase[ri] : L.dep[ri];
+        float d = base + dz;
+        d = (d > 20.0f) ? 1.0f : d;
+        L.dep[ri] = (float)fmax((double)d, 1e-4);
+      }
+      __syncthreads();
+    }
+    // ---- linearise + assemble this workgroup's block ----
+    double acc[36];
+    double* part = A.part + (size_t)g * kPart;
+    double* red = reinterpret_cast<double*>(L.region);
+    if (NB == 0) {
+      assemble<0>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, acc);
+    } else if (diag) {
+      assemble<1>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, acc);
+      reduce_acc<27>(acc, red, part);
+    } else {
+      assemble<2>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, acc);
+      reduce_acc<36>(acc, red, part);
+    }
+    mark(A, mb + 0);
+    if (NB == 0) continue;  // structure only: dZ = Q u, applied after the loop
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __hip_atomic_store(&A.flags[g], epoch * 64 + it + 1, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- wait for every partial, gather S and y in a fixed order ----
+    if (tid < 64) {
+      bool ok = true;
+      for (int w = tid; w < A.G; w += 64) ok = wait_flag(&A.flags[w], epoch * 64 + it + 1) && ok;
+      if (!ok) ctl[cTimeout] = 1;
+      // no acquire fence (it would invalidate this XCD's L2 under every one of
+      // the G workgroups): the partials are read below with agent-scope atomic
+      // loads, which go to the coherence point, issued after the flags were seen
+    }
+    __syncthreads();
+    mark(A, mb + 1);
+    const int NNb = N;
+    double* Sd = reinterpret_cast<double*>(L.region);
+    double* yd = Sd + 36 * NB;
+    double* pc = yd + 6 * N;  // [G][kPart] copy of the partials
+    {
+      const int tot_p = kPart * A.G;
+      constexpr int kIn = 8;  // loads in flight per thread
+      for (int t0_ = tid; t0_ < tot_p; t0_ += kIn * kWT) {
+        double v[kIn];
+#pragma unroll
+        for (int r = 0; r < kIn; r++) {
+          const int t = t0_ + r * kWT;
+          v[r] = (t < tot_p) ? __hip_atomic_load(A.part + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < kIn; r++)
+          if (t0_ + r * kWT < tot_p) pc[t0_ + r * kWT] = v[r];
+      }
+    }
+    __syncthreads();
+    for (int t = tid; t < 36 * NB; t += kWT) {
+      const int blk = t / 36, k = t % 36;
+      const int ba_ = L.tri[blk] >> 8, bb_ = L.tri[blk] & 0xff;
+      double s = 0.0;
+      if (ba_ == bb_) {  // diagonal: 21 lower entries stored; mirror
+        const int x = k / 6, z = k % 6;
+        const int xx = x >= z ? x : z, zz = x >= z ? z : x;
+        const int li = xx * (xx + 1) / 2 + zz;
+        for (int sb = 0; sb < A.Sd; sb++) s += pc[(ba_ * A.Sd + sb) * kPart + li];
+        if (x == z) s += 1e-4 * s + 1.0;  // S += I (1e-4 S + 1) (ba_cuda.cu:560)
+      } else {
+        const int o = ba_ * (ba_ - 1) / 2 + bb_;
+        const int g0 = NNb * A.Sd + o * A.So;
+        for (int sb = 0; sb < A.So; sb++) s += pc[(g0 + sb) * kPart + k];
+      }
+      Sd[t] = s;
+    }
+    for (int t = tid; t < 6 * N; t += kWT) {
+      const int i = t / 6, x = t % 6;
+      double s = 0.0;
+      for (int sb = 0; sb < A.Sd; sb++) s += pc[(i * A.Sd + sb) * kPart + 21 + x];
+      yd[t] = s;
+    }
+    __syncthreads();
+    mark(A, mb + 2);
+    // ---- dense solve, redundantly in every workgroup (identical bits) ----
+    WSolve sv;
+    sv.S = Sd;
+    sv.y = yd;
+    sv.x = yd + 6 * N;
+    sv.r = sv.x + 6 * N;
+    sv.A = reinterpret_cast<float*>(sv.r + 6 * N);
+    sv.Z = sv.A + 36 * NB;
+    sv.v0 = sv.Z + 36 * NB;
+    sv.v1 = sv.v0 + 6 * N;
+    const bool ok = wsolve(sv, N, kRefine, &ctl[cFail]);
+    const bool zero = !ok || ctl[cTimeout] != 0;
+    for (int k = tid; k < 6 * N; k += kWT) L.dX[k] = zero ? 0.0 : sv.x[k];  // (dpvo/ba.py:17-21)
+    if (!ok && g == 0 && tid == 0) atomicOr(A.status, kStChol);
+    __syncthreads();
+    mark(A, mb + 3);
+  }
+
+  // ---------------- final apply + write-back ----------------
+  if (A.iters > 0) {
+    const int it = A.iters;
+    for (int i = tid; i < N; i += kWT) {
+      float xi[6], tt[3], qq[4], t1[3], q1[4];
+#pragma unroll
+      for (int k = 0; k < 6; k++) xi[k] = (float)L.dX[6 * i + k];
+      float* pl = L.pose + 8 * i;
+      tt[0] = pl[0]; tt[1] = pl[1]; tt[2] = pl[2];
+      qq[0] = pl[3]; qq[1] = pl[4]; qq[2] = pl[5]; qq[3] = pl[6];
+      retrSE3(xi, tt, qq, t1, q1);
+      pl[0] = t1[0]; pl[1] = t1[1]; pl[2] = t1[2];
+      pl[3] = q1[0]; pl[4] = q1[1]; pl[5] = q1[2]; pl[6] = q1[3];
+    }
+    for (int ri = tid; ri < nrel_e; ri += kWT) {
+      if (L.pkx[ri] < 0) continue;
+      double ex = 0.0;
+      for (int q = L.roff[ri]; q < L.roff[ri + 1]; q++) {
+        const unsigned c = L.ec[q];
+        const unsigned si = c & 0xff, sj = c >> 8;
+        const float4* e4 = reinterpret_cast<const float4*>(L.ej + 12 * (size_t)q);
+        const float4 e0 = e4[0], e1 = e4[1], e2 = e4[2];
+        if (sj < (unsigned)N) {
+          const double* d = L.dX + 6 * sj;
+          ex += (double)e0.x * d[0] + (double)e0.y * d[1] + (double)e0.z * d[2] +
+                (double)e0.w * d[3] + (double)e1.x * d[4] + (double)e1.y * d[5];
+        }
+        if (si < (unsigned)N) {
+          const double* d = L.dX + 6 * si;
+          ex += (double)e1.z * d[0] + (double)e1.w * d[1] + (double)e2.x * d[2] +
+                (double)e2.y * d[3] + (double)e2.z * d[4] + (double)e2.w * d[5];
+        }
+      }
+      const double2 qu = L.qu[ri];
+      const float dz = (float)(qu.x * (qu.y - ex));
+      const float base = (it == 1) ? L.dbase[ri] : L.dep[ri];
+      float d = base + dz;
+      d = (d > 20.0f) ? 1.0f : d;
+      L.dep[ri] = (float)fmax((double)d, 1e-4);
+    }
+    __syncthreads();
+    for (int k = tid; k < nrel_e * PP; k += kWT) {
+      const int ri = k / PP, c = k % PP;
+      const int kx = L.pkx[ri];
+      if (kx >= 0) A.patches[(size_t)kx * 3 * PP + 2 * PP + c] = L.dep[ri];
+    }
+    if (g == 0)
+      for (int i = tid; i < N; i += kWT) {
+        const int gp = A.t0 + i;
+        if (gp >= 0 && gp < A.num_poses)
+          for (int c = 0; c < 7; c++) A.poses[7 * (size_t)gp + c] = L.pose[8 * i + c];
+      }
+  }
+  if (tid == 0) {
+    int st = 0;
+    if (ctl[cTimeout]) st |= kStTimeout;
+    if (g == 0) st |= A.plan.meta[2];  // kk clamp from the plan
+    if (st) atomicOr(A.status, st);
+    if (g == 0) {
+      __hip_atomic_store(&A.flags[kEpochWord], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      mark(A, 63);
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host side
+static size_t al256w(size_t v) { return (v + 255) / 256 * 256; }
+
+struct WGrid {
+  int NB, Sd, So, G;
+};
+static WGrid window_grid(int E, int N) {
+  WGrid w;
+  w.NB = N * (N + 1) / 2;
+  if (N <= 0) {
+    w.Sd = w.So = 1;
+    w.G = 1;
+    return w;
+  }
+  w.So = E > 2048 ? 2 : 1;
+  w.Sd = 4 * w.So;
+  auto G = [&]() { return N * w.Sd + (w.NB - N) * w.So; };
+  while (G() > kWMaxG && w.Sd > 1) {
+    if (w.Sd > w.So) w.Sd--;
+    else if (w.So > 1) w.So--;
+    else w.Sd--;
+  }
+  w.G = G();
+  return w;
+}
+
+bool ba_window_supported(int E, int N, int P) {
+  if (E <= 0 || E > kWMaxE || N < 0 || N > kWMaxN || P < 2 || P * P > 64) return false;
+  return window_grid(E, N).G <= kWMaxG;
+}
+
+size_t ba_window_scratch_bytes(int E, int N) {
+  const WGrid w = window_grid(E, N);
+  return al256w(sizeof(int) * (size_t)E) + al256w(sizeof(int) * (size_t)(E + 1)) +
+         al256w(sizeof(unsigned) * (size_t)E) + al256w(sizeof(int) * (size_t)E) +
+         al256w(sizeof(int) * 8) + al256w(sizeof(double) * kPart * (size_t)w.G) +
+         al256w(sizeof(float) * 16 * (size_t)w.G * E);
+}
+
+namespace {
+std::mutex g_wflag_mu;
+std::map<int, long long*> g_wflags;  // per device; BA calls on one device must not overlap
+long long* wflag_slot(hipStream_t st) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_wflag_mu);
+  auto it = g_wflags.find(dev);
+  if (it != g_wflags.end()) return it->second;
+  long long* p = nullptr;
+  if (hipMalloc(&p, sizeof(long long) * kFlagWords) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, sizeof(long long) * kFlagWords, st) != hipSuccess) return nullptr;
+  g_wflags[dev] = p;
+  return p;
+}
+}  // namespace
+
+int ba_window_launch(float* poses, float* patches, const float* intrinsics, const float* target,
+                     const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
+                     const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
+                     int iterations, char* scratch, int* status, int64_t* marks, void* stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)ba_window_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
+    (void)hipFuncSetAttribute((const void*)ba_plan_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
+    attr = true;
+  }
+  if (iterations > 63) return DPVO_ERR_UNSUPPORTED;  // 6-bit iteration tag per epoch
+  const int N = t1 - t0;
+  const WGrid w = window_grid(E, N);
+  hipStream_t st = as_stream(stream);
+  WArgs a;
+  a.flags = wflag_slot(st);
+  if (!a.flags) return DPVO_ERR_LAUNCH;
+  char* s = scratch;
+  a.plan.epos = (int*)s;
+  s += al256w(sizeof(int) * (size_t)E);
+  a.plan.poff = (int*)s;
+  s += al256w(sizeof(int) * (size_t)(E + 1));
+  a.plan.pmask = (unsigned*)s;
+  s += al256w(sizeof(unsigned) * (size_t)E);
+  a.plan.pkk = (int*)s;
+  s += al256w(sizeof(int) * (size_t)E);
+  a.plan.meta = (int*)s;
+  s += al256w(sizeof(int) * 8);
+  a.part = (double*)s;
+  s += al256w(sizeof(double) * kPart * (size_t)w.G);
+  a.ejg = (float*)s;
+  a.poses = poses;
+  a.patches = patches;
+  a.intrinsics = intrinsics;
+  a.target = target;
+  a.weight = weight;
+  a.lmbda = lmbda;
+  a.ii = ii;
+  a.jj = jj;
+  a.kk = kk;
+  a.E = E;
+  a.P = P;
+  a.num_poses = num_poses;
+  a.num_patches = num_patches;
+  a.t0 = t0;
+  a.N = N;
+  a.iters = iterations;
+  a.NB = w.NB;
+  a.Sd = w.Sd;
+  a.So = w.So;
+  a.G = w.G;
+  a.status = status;
+  a.marks = marks;
+  if (hipMemsetAsync(status, 0, sizeof(int), st) != hipSuccess) return DPVO_ERR_LAUNCH;
+  hipLaunchKernelGGL(ba_plan_kernel, dim3(1), dim3(kPT), kWLds, st, ii, jj, kk, E, num_patches,
+                     num_poses, t0, N, a.plan);
+  int rc = launch_status();
+  if (rc) return rc;
+  hipLaunchKernelGGL(ba_window_kernel, dim3(w.G), dim3(kWT), kWLds, st, a);
+  return launch_status();
+}
+
+}  // namespace dpvo

@@ -29,7 +29,7 @@ static torch::Tensor f32_contig(const torch::Tensor& t, const char* name) {
 // surface at most one call late, like an asynchronous HIP error.
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kFatalBits = 2 | 4 | 8 | 16;
+constexpr int kFatalBits = 2 | 4 | 8 | 16 | 32;
 struct StatusSlot {
   torch::Tensor acc;     // device int32 [1], sticky OR of all statuses
   int* host = nullptr;   // pinned copy
@@ -47,6 +47,7 @@ std::string describe_status(int s) {
   if (s & 4) m += " [4: a patch touches more free poses than the large-graph solver handles]";
   if (s & 8) m += " [8: too many border poses for the large-graph solver]";
   if (s & 16) m += " [16: cross-workgroup wait timed out]";
+  if (s & 32) m += " [32: window graph exceeds the per-workgroup LDS capacity]";
   return m;
 }
 
@@ -270,15 +271,32 @@ std::vector<torch::Tensor> ba_neighbors(torch::Tensor ii, torch::Tensor jj) {
 }
 
 // ba.cpp:120-180: Sim3 pose-graph solve of the loop-closure backend
-// (optim_utils.py:229).  Assembly of A = J^T J (+ damping) and b = -J^T res on
-// the device (pgo.hip, fp64 like the reference's Eigen system); the SPD solve of
-// the top-left freen*7 block by the device Cholesky in fp64; delta returned as
-// f32 [n, 7] with the rows of fixed poses zero (ba.cpp:103-118).
+// (optim_utils.py:229).  Like the reference it accepts tensors on any device
+// and returns delta on res.device() (ba.cpp:123-129, 170): host inputs (the
+// loop-closure worker runs perform_updates on CPU tensors, long_term.py:258)
+// are copied to the current HIP device, solved there, and copied back.
+// Assembly of A = J^T J (+ damping) and b = -J^T res on the device (pgo.hip,
+// fp64 like the reference's Eigen system); the SPD solve of the top-left
+// freen*7 block by the device Cholesky in fp64; delta returned as f32 [n, 7]
+// with the rows of fixed poses zero (ba.cpp:103-118).  A factorisation that
+// fails (NaN / not positive definite) raises RuntimeError instead of
+// returning garbage (the reference leaves Eigen's info unchecked).
 std::vector<torch::Tensor> ba_solve_system(torch::Tensor J_Ginv_i, torch::Tensor J_Ginv_j,
                                            torch::Tensor ii, torch::Tensor jj, torch::Tensor res,
                                            double ep, double lm, int freen) {
-  check_device(res, "res");
-  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(res.device());
+  const torch::Device out_dev = res.device();
+  torch::Device dev = out_dev;
+  if (!res.is_cuda()) {
+    TORCH_CHECK(torch::cuda::is_available(),
+                "cuda_ba.solve_system: no HIP device (the MI355X build has no CPU path)");
+    dev = torch::Device(torch::kCUDA, c10::hip::current_device());
+  }
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(dev);
+  J_Ginv_i = J_Ginv_i.to(dev);
+  J_Ginv_j = J_Ginv_j.to(dev);
+  ii = ii.to(dev);
+  jj = jj.to(dev);
+  res = res.to(dev);
   J_Ginv_i = f32_contig(J_Ginv_i, "J_Ginv_i");
   J_Ginv_j = f32_contig(J_Ginv_j, "J_Ginv_j");
   res = f32_contig(res, "res");
@@ -312,10 +330,15 @@ std::vector<torch::Tensor> ba_solve_system(torch::Tensor J_Ginv_i, torch::Tensor
   auto delta = torch::zeros({7 * n}, opt64);
   if (f > 0) {
     auto As = A.narrow(0, 0, f).narrow(1, 0, f);
-    auto L = std::get<0>(at::linalg_cholesky_ex(As));
-    delta.narrow(0, 0, f).copy_(at::cholesky_solve(b.narrow(0, 0, f).unsqueeze(1), L).squeeze(1));
+    auto chol = at::linalg_cholesky_ex(As);
+    const int64_t info = std::get<1>(chol).item<int64_t>();
+    TORCH_CHECK(info == 0, "cuda_ba.solve_system: the damped pose-graph system is not positive "
+                "definite (Cholesky info ", info, "); check for NaN residuals/Jacobians or "
+                "unconstrained poses with ep = 0");
+    delta.narrow(0, 0, f).copy_(
+        at::cholesky_solve(b.narrow(0, 0, f).unsqueeze(1), std::get<0>(chol)).squeeze(1));
   }
-  return {delta.to(torch::kFloat32).view({n, 7})};
+  return {delta.to(torch::kFloat32).view({n, 7}).to(out_dev)};
 }
 
 // Split F-BA for the edge-sharded multi-GPU path.
@@ -480,7 +503,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("reproject_ordered", &ba_reproject_ordered,
         "reproject + edge order by target frame (for cuda_corr.forward_levels(order=))");
   m.def("select_path", [](int mode) { check_status(dpvo_ba_select_path(mode), "select_path"); },
-        "F-BA implementation: 0 auto, 1 fused single workgroup, 2 multi-kernel, 3 blocks, 4 large-graph");
+        "F-BA implementation: 0 auto, 1 fused single workgroup, 2 multi-kernel, 3 blocks, 4 large-graph, 5 window");
   m.def("set_refine", [](int on) { check_status(dpvo_ba_set_refine(on), "set_refine"); },
         "dense pose solve: 2 = fp64 block LDL^T (default), 0 = fp32 Cholesky (reference precision), 1 = fp32 + one fp64 refinement step");
   m.attr("native_library") = dpvo_version();

@@ -201,8 +201,8 @@ int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1, int* out, 
    (sticky; the caller resets it).  Bits: 1 Cholesky failed (dX = 0, as
    dpvo/ba.py:17-21), 2 kk outside [0, num_patches) (clamped), 4 a patch
    touches more free poses than the large-graph solver handles, 8 too many
-   border poses (large graph), 16 a cross-workgroup wait timed out.  Bits
-   2..16 mean the step was not the reference's and the extension raises.
+   border poses (large graph), 16 a cross-workgroup wait timed out, 32 a
+   window graph too large for the per-workgroup LDS plan.  Bits 2..32 mean the step was not the reference's and the extension raises.
    Graph-capturable (one tiny kernel, no host sync). */
 int dpvo_ba_status_accumulate(const void* workspace, int E, int t0, int t1, int* acc,
                               void* stream);

@@ -1,0 +1,60 @@
+"""Per-phase timing of the default F-BA path (ba_window.hip) from the
+wall-clock stamps (100 MHz) workgroup 0 leaves: [0] start, [1] setup done,
+per iteration (mb = 2 + 8 it): mb+0 block assembled + reduced + stored,
+mb+1 every partial arrived, mb+2 S gathered, mb+3 solved; [63] end.
+The plan kernel runs before [0] (its time is in 'call - kernel').
+
+    python scripts/ba_window_phases.py [cfg|M] [iterations]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import torch  # noqa: E402
+
+import dpvo_amd  # noqa: E402
+from dpvo_amd import synthetic  # noqa: E402
+
+cb = dpvo_amd.load_extension("cuda_ba")
+dev = torch.device("cuda:0")
+arg = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
+iters = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+if arg.startswith("cfg"):
+    G = synthetic.make_config(arg, seed=0)
+    t0, t1 = 1, G.F
+else:
+    G = synthetic.make_dpvo_window(M=int(arg), seed=int(arg))
+    t0, t1 = G.F - 10, G.F
+D = G.to(dev)
+lm = torch.tensor([1e-4], device=dev)
+acc = {}
+for rep in range(40):
+    poses, patches = D.poses.clone(), D.patches.clone()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    cb.forward(poses, patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj, D.kk, G.M, t0, t1,
+               iters, False)
+    e1.record()
+    torch.cuda.synchronize()
+    poses, patches = D.poses.clone(), D.patches.clone()
+    m = cb.forward_marks(poses, patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj, D.kk,
+                         G.M, t0, t1, iters, False).cpu().tolist()
+    if rep < 5:
+        continue
+    d = {"call (events)": e0.elapsed_time(e1) * 1e3, "kernel (marks)": (m[63] - m[0]) * 0.01,
+         "setup": (m[1] - m[0]) * 0.01}
+    prev = 1
+    for it in range(iters):
+        mb = 2 + 8 * it
+        d[f"it{it}: (apply+) assemble+reduce"] = (m[mb] - m[prev]) * 0.01
+        d[f"it{it}: wait partials"] = (m[mb + 1] - m[mb]) * 0.01
+        d[f"it{it}: gather"] = (m[mb + 2] - m[mb + 1]) * 0.01
+        d[f"it{it}: solve"] = (m[mb + 3] - m[mb + 2]) * 0.01
+        prev = mb + 3
+    d["final apply + write-back"] = (m[63] - m[prev]) * 0.01
+    for k, v in d.items():
+        acc.setdefault(k, []).append(v)
+print(f"{arg}: E={G.E} N={t1 - t0} iterations={iters}")
+for k, v in acc.items():
+    v = sorted(v)
+    print(f"{k:34s} median {v[len(v) // 2]:8.2f} us")

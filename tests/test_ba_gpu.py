@@ -23,11 +23,12 @@ def cb(gpu):
     return dpvo_amd.load_extension("cuda_ba")
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["blocks", "fused", "multikernel"])
+@pytest.fixture(params=[0, 1, 2, 3], ids=["window", "fused", "multikernel", "blocks"])
 def path(request, cb):
-    """F-BA implementation under test: 0 = auto (one persistent workgroup per
-    block of S for these window sizes), 1 = the single-workgroup kernel,
-    2 = the multi-kernel path."""
+    """F-BA implementation under test: 0 = auto (ba_window.hip: plan kernel +
+    one persistent workgroup per share of a block of S, solve in every
+    workgroup), 1 = the single-workgroup kernel, 2 = the multi-kernel path,
+    3 = the round-1 per-block kernel (ba_blocks.hip)."""
     cb.select_path(request.param)
     yield request.param
     cb.select_path(0)
@@ -108,8 +109,9 @@ def test_ba_is_deterministic(cb, gpu):
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
-def test_blocks_path_is_deterministic(cb, gpu):
-    # per-block workgroups reduce in a fixed order: bit-identical reruns
+def test_window_path_is_deterministic(cb, gpu):
+    # per-block workgroups reduce in a fixed order, every workgroup sums the
+    # partials in the same order: bit-identical reruns
     G = synthetic.make_config("cfg2", seed=3)
     a = _run_gpu(cb, G, gpu, 1, G.F, 2)
     b = _run_gpu(cb, G, gpu, 1, G.F, 2)
