@@ -87,6 +87,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="run the BA edge grouping inline instead of on a side stream "
+                         "concurrently with A-CORR")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python each step (default: replay the "
                          "step as one captured hipGraph)")
@@ -129,7 +132,20 @@ def main():
     jj1 = D.jj % args.mem
     scales = [float(s) for s in levels]
 
+    plan_stream = torch.cuda.Stream()
+
     def step(i=0, ev=None):
+        cur = torch.cuda.current_stream()
+        ws = None
+        if not args.no_overlap:
+            # the BA edge grouping reads the patch graph only (fixed before the
+            # update, dpvo.py:775-824): issue it on a side stream so it runs
+            # concurrently with the frame insertion / reprojection / A-CORR
+            plan_stream.wait_stream(cur)
+            with torch.cuda.stream(plan_stream):
+                ws = fastba.plan(D.ii, D.jj, D.kk, 1, G.F, patches.shape[0], poses.shape[0], P)
+            if ws is not None:
+                ws.record_stream(cur)
         slot = i % args.mem  # frame insertion (dpvo.py:__call__ -> ring buffer)
         altcorr.insert_frame(pyr_nchw[0][0, slot], pyr, slot, levels)
         # reprojection + the XCD-aware edge order (edges grouped by target
@@ -141,8 +157,10 @@ def main():
         corr = altcorr.corr_levels(gbuf, pyr, coords, kk1, jj1, 3, scales, order=order)
         if ev is not None:
             ev[1].record()
+        if not args.no_overlap:
+            cur.wait_stream(plan_stream)
         fastba.BA(poses, patches, D.intrinsics, D.target, D.weight, lmbda, D.ii, D.jj, D.kk, 1,
-                  G.F, M=G.M, iterations=args.ba_iters)
+                  G.F, M=G.M, iterations=args.ba_iters, plan=ws)
         return corr
 
     for i in range(args.warmup):
@@ -233,6 +251,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic (SURVEY 8d cfg2 recipe, seeded)",
             "launch": "eager" if graph is None else "hipGraph replay of one captured step",
+            "ba_plan": "inline" if args.no_overlap else "side stream, concurrent with A-CORR",
             "config": {
                 "workload": f"{args.config}: {G.M} patches/frame x {G.E} edges, p={P}, "
                             f"{len(levels)}-level pyramid {levels}, fp32, BA {args.ba_iters} iters",

@@ -1083,6 +1083,12 @@ int ba_window_launch(float* poses, float* patches, const float* intrinsics, cons
                      const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                      const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
                      int iterations, char* scratch, int* status, int64_t* marks, void* stream);
+int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
+                   int num_poses, int t0, int t1, char* scratch, int* status, void* stream);
+int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
+                  const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
+                  const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
+                  int iterations, char* scratch, int* status, int64_t* marks, void* stream);
 // ba_large.hip: large graphs (global BA, cfg4)
 size_t gba_workspace_bytes(int E, int N);
 int gba_forward(float* poses, float* patches, const float* intrinsics, const float* target,
@@ -1359,6 +1365,43 @@ DPVO_EXPORT int dpvo_ba_forward(float* poses, float* patches, const float* intri
     st = launch_status();
   }
   return st;
+}
+
+DPVO_EXPORT int dpvo_ba_plan_supported(int E, int t0, int t1, int P) {
+  return (g_ba_path == 0 || g_ba_path == 5) && ba_window_supported(E, t1 - t0, P) ? 1 : 0;
+}
+
+DPVO_EXPORT int dpvo_ba_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E,
+                             int num_patches, int num_poses, int t0, int t1, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  if (E <= 0) return DPVO_OK;
+  if (!ii || !jj || !kk || !workspace || num_patches <= 0 || num_poses <= 0 || t1 < t0)
+    return DPVO_ERR_INVALID;
+  if (!ba_window_supported(E, t1 - t0, 3)) return DPVO_ERR_UNSUPPORTED;
+  if (workspace_bytes < dpvo_ba_workspace_bytes(E, t0, t1)) return DPVO_ERR_WORKSPACE;
+  BaWs w;
+  const size_t base_bytes = ba_layout(E, t1 - t0, (char*)workspace, &w);
+  return ba_window_plan(ii, jj, kk, E, num_patches, num_poses, t0, t1,
+                        (char*)workspace + base_bytes, w.meta + 1, stream);
+}
+
+DPVO_EXPORT int dpvo_ba_forward_planned(float* poses, float* patches, const float* intrinsics,
+                                        const float* target, const float* weight,
+                                        const float* lmbda, const int64_t* ii, const int64_t* jj,
+                                        const int64_t* kk, int E, int P, int num_poses,
+                                        int num_patches, int t0, int t1, int iterations,
+                                        void* workspace, size_t workspace_bytes, void* stream) {
+  if (E <= 0 || iterations <= 0) return DPVO_OK;
+  if (P < 2 || num_poses <= 0 || num_patches <= 0 || t1 < t0 || !workspace || !poses ||
+      !patches || !intrinsics || !target || !weight || !lmbda || !ii || !jj || !kk)
+    return DPVO_ERR_INVALID;
+  if (!ba_window_supported(E, t1 - t0, P)) return DPVO_ERR_UNSUPPORTED;
+  if (workspace_bytes < dpvo_ba_workspace_bytes(E, t0, t1)) return DPVO_ERR_WORKSPACE;
+  BaWs w;
+  const size_t base_bytes = ba_layout(E, t1 - t0, (char*)workspace, &w);
+  return ba_window_run(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
+                       num_poses, num_patches, t0, t1, iterations, (char*)workspace + base_bytes,
+                       w.meta + 1, w.tmark, stream);
 }
 
 DPVO_EXPORT int dpvo_reproject(const float* poses, const float* patches, const float* intrinsics,

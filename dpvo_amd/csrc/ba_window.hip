@@ -65,6 +65,7 @@ struct Plan {          // written by ba_plan_kernel, read by ba_window_kernel
   unsigned* pmask;     // [E] free-pose bitmask of patch u
   int* pkk;            // [E] patch id (kk) of patch u
   int* meta;           // [8] nuniq, fmin, status
+  int* status;         // the workspace status word, reset here
 };
 
 struct WArgs {
@@ -269,6 +270,7 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
     plan.meta[0] = nuniq;
     plan.meta[1] = ctl[2];
     plan.meta[2] = ctl[3];
+    *plan.status = 0;  // this call's status word (ORed by the iteration kernel)
   }
 }
 
@@ -915,10 +917,23 @@ long long* wflag_slot(hipStream_t st) {
 }
 }  // namespace
 
-int ba_window_launch(float* poses, float* patches, const float* intrinsics, const float* target,
-                     const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
-                     const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
-                     int iterations, char* scratch, int* status, int64_t* marks, void* stream) {
+static Plan plan_view(char* scratch, int E, int* status) {
+  Plan p;
+  char* s = scratch;
+  p.epos = (int*)s;
+  s += al256w(sizeof(int) * (size_t)E);
+  p.poff = (int*)s;
+  s += al256w(sizeof(int) * (size_t)(E + 1));
+  p.pmask = (unsigned*)s;
+  s += al256w(sizeof(unsigned) * (size_t)E);
+  p.pkk = (int*)s;
+  s += al256w(sizeof(int) * (size_t)E);
+  p.meta = (int*)s;
+  p.status = status;
+  return p;
+}
+
+static void set_attrs() {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)ba_window_kernel,
@@ -927,6 +942,40 @@ int ba_window_launch(float* poses, float* patches, const float* intrinsics, cons
                               hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
     attr = true;
   }
+}
+
+// edge grouping only (reads ii / jj / kk): may run on another stream than
+// the iterations, e.g. concurrently with A-CORR
+int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
+                   int num_poses, int t0, int t1, char* scratch, int* status, void* stream) {
+  set_attrs();
+  const Plan plan = plan_view(scratch, E, status);
+  hipLaunchKernelGGL(ba_plan_kernel, dim3(1), dim3(kPT), kWLds, as_stream(stream), ii, jj, kk, E,
+                     num_patches, num_poses, t0, t1 - t0, plan);
+  return launch_status();
+}
+
+int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
+                  const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
+                  const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
+                  int iterations, char* scratch, int* status, int64_t* marks, void* stream);
+
+int ba_window_launch(float* poses, float* patches, const float* intrinsics, const float* target,
+                     const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
+                     const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
+                     int iterations, char* scratch, int* status, int64_t* marks, void* stream) {
+  const int rc = ba_window_plan(ii, jj, kk, E, num_patches, num_poses, t0, t1, scratch, status,
+                                stream);
+  if (rc) return rc;
+  return ba_window_run(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
+                       num_poses, num_patches, t0, t1, iterations, scratch, status, marks, stream);
+}
+
+int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
+                  const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
+                  const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
+                  int iterations, char* scratch, int* status, int64_t* marks, void* stream) {
+  set_attrs();
   if (iterations > 63) return DPVO_ERR_UNSUPPORTED;  // 6-bit iteration tag per epoch
   const int N = t1 - t0;
   const WGrid w = window_grid(E, N);
@@ -934,17 +983,10 @@ int ba_window_launch(float* poses, float* patches, const float* intrinsics, cons
   WArgs a;
   a.flags = wflag_slot(st);
   if (!a.flags) return DPVO_ERR_LAUNCH;
-  char* s = scratch;
-  a.plan.epos = (int*)s;
-  s += al256w(sizeof(int) * (size_t)E);
-  a.plan.poff = (int*)s;
-  s += al256w(sizeof(int) * (size_t)(E + 1));
-  a.plan.pmask = (unsigned*)s;
-  s += al256w(sizeof(unsigned) * (size_t)E);
-  a.plan.pkk = (int*)s;
-  s += al256w(sizeof(int) * (size_t)E);
-  a.plan.meta = (int*)s;
-  s += al256w(sizeof(int) * 8);
+  a.plan = plan_view(scratch, E, status);
+  char* s = scratch + al256w(sizeof(int) * (size_t)E) + al256w(sizeof(int) * (size_t)(E + 1)) +
+            al256w(sizeof(unsigned) * (size_t)E) + al256w(sizeof(int) * (size_t)E) +
+            al256w(sizeof(int) * 8);
   a.part = (double*)s;
   s += al256w(sizeof(double) * kPart * (size_t)w.G);
   a.ejg = (float*)s;
@@ -970,11 +1012,6 @@ int ba_window_launch(float* poses, float* patches, const float* intrinsics, cons
   a.G = w.G;
   a.status = status;
   a.marks = marks;
-  if (hipMemsetAsync(status, 0, sizeof(int), st) != hipSuccess) return DPVO_ERR_LAUNCH;
-  hipLaunchKernelGGL(ba_plan_kernel, dim3(1), dim3(kPT), kWLds, st, ii, jj, kk, E, num_patches,
-                     num_poses, t0, N, a.plan);
-  int rc = launch_status();
-  if (rc) return rc;
   hipLaunchKernelGGL(ba_window_kernel, dim3(w.G), dim3(kWT), kWLds, st, a);
   return launch_status();
 }

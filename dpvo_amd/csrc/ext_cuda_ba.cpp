@@ -186,6 +186,63 @@ std::vector<torch::Tensor> ba_forward(torch::Tensor poses, torch::Tensor patches
   return {};
 }
 
+// Split call (dpvo_ba_plan / dpvo_ba_forward_planned): plan(...) -> workspace,
+// reads ii / jj / kk only (may run on a side stream concurrently with A-CORR);
+// forward_planned(ws, ...) runs the iterations.  Same results as forward().
+bool ba_plan_supported(int E, int t0, int t1, int P) { return dpvo_ba_plan_supported(E, t0, t1, P); }
+
+torch::Tensor ba_plan(torch::Tensor ii, torch::Tensor jj, torch::Tensor kk, int64_t num_patches,
+                      int64_t num_poses, int t0, int t1) {
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  kk = idx64(kk, "kk");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ii.device());
+  const int E = ii.numel();
+  TORCH_CHECK(jj.numel() == E && kk.numel() == E, "ii, jj, kk must have equal length");
+  const size_t wsb = dpvo_ba_workspace_bytes(E, t0, t1);
+  auto ws = torch::empty({(int64_t)wsb}, ii.options().dtype(torch::kUInt8));
+  check_status(dpvo_ba_plan(ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), kk.data_ptr<int64_t>(),
+                            E, (int)num_patches, (int)num_poses, t0, t1, ws.data_ptr(), wsb,
+                            current_stream()),
+               "cuda_ba.plan");
+  return ws;
+}
+
+void ba_forward_planned(torch::Tensor ws, torch::Tensor poses, torch::Tensor patches,
+                        torch::Tensor intrinsics, torch::Tensor target, torch::Tensor weight,
+                        torch::Tensor lmbda, torch::Tensor ii, torch::Tensor jj, torch::Tensor kk,
+                        int t0, int t1, int iterations) {
+  check_device(poses, "poses");
+  check_device(patches, "patches");
+  TORCH_CHECK(poses.scalar_type() == torch::kFloat32 && patches.scalar_type() == torch::kFloat32,
+              "poses / patches must be float32");
+  TORCH_CHECK(poses.is_contiguous() && patches.is_contiguous(),
+              "poses and patches must be contiguous (updated in place)");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  const int P = patches.size(-1);
+  const int num_poses = poses.numel() / 7;
+  const int num_patches = patches.numel() / (3 * P * P);
+  intrinsics = f32_contig(intrinsics, "intrinsics");
+  target = f32_contig(target, "target");
+  weight = f32_contig(weight, "weight");
+  lmbda = f32_contig(lmbda, "lmbda");
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  kk = idx64(kk, "kk");
+  const int E = ii.numel();
+  TORCH_CHECK(target.numel() >= 2 * E && weight.numel() >= 2 * E, "target/weight must be [.., E, 2]");
+  if (E == 0 || iterations <= 0) return;
+  poll_status(poses);
+  check_status(dpvo_ba_forward_planned(poses.data_ptr<float>(), patches.data_ptr<float>(),
+                                       intrinsics.data_ptr<float>(), target.data_ptr<float>(),
+                                       weight.data_ptr<float>(), lmbda.data_ptr<float>(),
+                                       ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(),
+                                       kk.data_ptr<int64_t>(), E, P, num_poses, num_patches, t0,
+                                       t1, iterations, ws.data_ptr(), ws.numel(), current_stream()),
+               "cuda_ba.forward_planned");
+  track_status(ws, poses, E, t0, t1);
+}
+
 // Same call; returns the 128 phase marks followed by the per-workgroup marks (100 MHz ticks:
 // start, setup, then linearize/patch/schur/solve/update per iteration).
 torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
@@ -490,6 +547,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("solve_update", &ba_solve_update, "Cholesky solve + pose/patch retraction");
   m.def("last_status", &ba_last_status, "status word of the last BA on a workspace");
   m.def("max_free_poses", &dpvo_ba_max_free_poses);
+  m.def("plan_supported", &ba_plan_supported, "window path available for (E, t0, t1, P)");
+  m.def("plan", &ba_plan, "group the edges by patch (reads ii/jj/kk only) -> workspace");
+  m.def("forward_planned", &ba_forward_planned, "BA iterations on a planned workspace");
   m.def("check_status", &ba_check_status,
         "sync on the BA status of every forward so far on the device of `like`; raises "
         "RuntimeError on fatal bits (2 bad kk, 4/8 large-graph limits, 16 timeout); returns "

@@ -16,12 +16,29 @@ cuda_ba = load_extension("cuda_ba")
 
 
 def BA(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, M, iterations,
-       eff_impl=False):
+       eff_impl=False, plan=None):
     """fastba.BA (dpvo/fastba/ba.py:7-8): note the extension's argument order
-    puts patches-per-frame (M) before t0 (ba.cpp:32-45)."""
+    puts patches-per-frame (M) before t0 (ba.cpp:32-45).  ``plan``: a
+    workspace from :func:`plan` for the same ii / jj / kk / t0 / t1 (the edge
+    grouping then is not redone here)."""
     data = poses.data if hasattr(poses, "data") else poses
+    if plan is not None:
+        cuda_ba.forward_planned(plan, data, patches, intrinsics, target, weight, lmbda, ii, jj, kk,
+                                t0, t1, iterations)
+        return []
     return cuda_ba.forward(data, patches, intrinsics, target, weight, lmbda, ii, jj, kk, M, t0, t1,
                            iterations, eff_impl)
+
+
+def plan(ii, jj, kk, t0, t1, num_patches, num_poses, P=3):
+    """Group the edges by patch for a later ``BA(..., plan=ws)`` with the same
+    graph.  Reads ii / jj / kk only, so DPVO can issue it on a side stream
+    while A-CORR runs (the patch graph is fixed before the update,
+    dpvo/dpvo.py:775-824).  Returns None when the window path does not cover
+    the shape (then BA() plans internally)."""
+    if not cuda_ba.plan_supported(int(ii.numel()), int(t0), int(t1), int(P)):
+        return None
+    return cuda_ba.plan(ii, jj, kk, int(num_patches), int(num_poses), int(t0), int(t1))
 
 
 def neighbors(ii, jj):
@@ -40,4 +57,4 @@ def reproject(poses, patches, intrinsics, ii, jj, kk, mem=None):
     return tuple(cuda_ba.reproject_ordered(poses, patches, intrinsics, ii, jj, kk, int(mem)))
 
 
-__all__ = ["BA", "neighbors", "reproject", "cuda_ba"]
+__all__ = ["BA", "plan", "neighbors", "reproject", "cuda_ba"]

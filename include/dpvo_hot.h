@@ -196,6 +196,24 @@ int dpvo_ba_solve_update(float* poses, float* patches, const double* S_lower, co
    `out`: bit 0 = Cholesky failed in the last solve (dX was set to 0),
    bit 1 = some kk outside [0, num_patches) (clamped). */
 int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1, int* out, void* stream);
+/* Split F-BA for a caller that knows the edge list before the update (DPVO
+   fixes the patch graph before reproject / corr, dpvo.py:775-824).
+   dpvo_ba_plan groups the edges by patch -- it reads ii / jj / kk only, so it
+   can run on a side stream concurrently with A-CORR -- and
+   dpvo_ba_forward_planned runs the iterations on that workspace (same
+   workspace size as dpvo_ba_forward; identical results).  Only for shapes
+   dpvo_ba_plan_supported() accepts (the window path: E <= 4096, N <= 16,
+   P * P <= 64); otherwise call dpvo_ba_forward. */
+int dpvo_ba_plan_supported(int E, int t0, int t1, int P);
+int dpvo_ba_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
+                 int num_poses, int t0, int t1, void* workspace, size_t workspace_bytes,
+                 void* stream);
+int dpvo_ba_forward_planned(float* poses, float* patches, const float* intrinsics,
+                            const float* target, const float* weight, const float* lmbda,
+                            const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int P,
+                            int num_poses, int num_patches, int t0, int t1, int iterations,
+                            void* workspace, size_t workspace_bytes, void* stream);
+
 /* OR the status word of the last dpvo_ba_forward on this workspace (any
    path: window kernels or the large-graph solver) into the DEVICE int `acc`
    (sticky; the caller resets it).  Bits: 1 Cholesky failed (dX = 0, as

@@ -53,6 +53,29 @@ def test_dpvo_window_matches_oracle(cb, gpu, M, iters):
     assert np.abs(P[t0:] - G.poses.numpy()[t0:]).max() > 1e-5
 
 
+@pytest.mark.parametrize("cfg", ["cfg1", "cfg2"])
+def test_planned_forward_is_bit_identical(cb, gpu, cfg):
+    """fastba.plan on a side stream + BA(plan=) == BA() (dpvo_ba_plan /
+    dpvo_ba_forward_planned vs dpvo_ba_forward)."""
+    from dpvo_amd import fastba
+
+    G = synthetic.make_config(cfg, seed=7)
+    D = G.to(gpu)
+    lm = torch.tensor([1e-4], device=gpu)
+    P0, K0 = _run(cb, G, gpu, 1, G.F, 2)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ws = fastba.plan(D.ii, D.jj, D.kk, 1, G.F, D.patches.shape[0], D.poses.shape[0])
+    assert ws is not None
+    torch.cuda.current_stream().wait_stream(side)
+    poses, patches = D.poses.clone(), D.patches.clone()
+    fastba.BA(poses, patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj, D.kk, 1, G.F,
+              M=G.M, iterations=2, plan=ws)
+    assert torch.equal(poses, P0) and torch.equal(patches, K0)
+    assert cb.check_status(poses) == 0
+
+
 def test_bad_patch_index_raises(cb, gpu):
     G = synthetic.make_config("cfg1", seed=3)
     G.kk = G.kk.clone()
