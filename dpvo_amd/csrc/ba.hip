@@ -1278,12 +1278,22 @@ __global__ void k_status_or(const int* src, int* acc) {
 }
 }  // namespace
 
+namespace dpvo {
+void ba_set_status_sink(int* sink);
+}
+DPVO_EXPORT int dpvo_ba_set_status_sink(int* acc) {
+  dpvo::ba_set_status_sink(acc);
+  return DPVO_OK;
+}
+
 DPVO_EXPORT int dpvo_ba_status_accumulate(const void* workspace, int E, int t0, int t1, int* acc,
                                           void* stream) {
   if (!workspace || !acc) return DPVO_ERR_INVALID;
   if (E <= 0) return DPVO_OK;
   const int N = t1 > t0 ? t1 - t0 : 0;
   if (use_large(E, N)) return gba_status_or(workspace, E, N, acc, stream);
+  // the window kernels OR their status into the registered sink themselves
+  if ((g_ba_path == 0 || g_ba_path == 5) && ba_window_supported(E, N, 3)) return DPVO_OK;
   BaWs w;
   ba_layout(E, N, (char*)workspace, &w);
   hipLaunchKernelGGL(k_status_or, dim3(1), dim3(64), 0, as_stream(stream), w.meta + 1, acc);

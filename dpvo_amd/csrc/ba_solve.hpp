@@ -161,6 +161,29 @@ __device__ __forceinline__ void row_sub_abt(float* out, const float* arow, const
   st_row(out, o);
 }
 
+// rows x and x+1 of a block at once: B (36 values) loaded once for both
+__device__ __forceinline__ void row2_sub_abt(float* out, const float* arow, const float* Bp) {
+  float a0[6], a1[6], o0[6], o1[6], B[36];
+  ld_row(arow, a0);
+  ld_row(arow + 6, a1);
+  ld_row(out, o0);
+  ld_row(out + 6, o1);
+  ld_blk(Bp, B);
+#pragma unroll
+  for (int z = 0; z < 6; z++) {
+    float s0 = o0[z], s1 = o1[z];
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      s0 -= a0[q] * B[6 * z + q];
+      s1 -= a1[q] * B[6 * z + q];
+    }
+    o0[z] = s0;
+    o1[z] = s1;
+  }
+  st_row(out, o0);
+  st_row(out + 6, o1);
+}
+
 // quad (4 adjacent lanes) sum
 __device__ __forceinline__ float quad_sum(float v) {
   v += __shfl_xor(v, 1, 64);
@@ -258,6 +281,8 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int NB = N * (N + 1) / 2, n = 6 * N;
   wstamp(st, 0);
+  // wave 0 carries the pivot chain: let it win issue / LDS arbitration
+  if (wid == 0) __builtin_amdgcn_s_setprio(3);
   for (int k = tid; k < 36 * NB; k += blockDim.x) {
     s.A[k] = (float)s.S[k];
     s.Z[k] = 0.0f;
@@ -315,19 +340,19 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
       const int t0 = tid - 64, T3 = blockDim.x - 64;
       // (5) trailing A_ij -= L_ik L_jk^T, k+2 <= j <= i
       const int m = N - k - 2;
-      const int n5 = m > 0 ? 6 * (m * (m + 1) / 2) : 0;
+      const int n5 = m > 0 ? 3 * (m * (m + 1) / 2) : 0;  // row pairs
       // (6) Z_kj = L_kk^-1 (T_kj - L_{k,k-1} Z_{k-1,j}) (j < k), Z_kk = L_kk^-1: column tasks
       const int n6 = 6 * (k + 1);
       // (7) T_ij -= L_{i,k-1} Z_{k-1,j}, i >= k+1, j <= k-1
       const int n7 = (k >= 1) ? 6 * (N - k - 1) * k : 0;
       for (int t = t0; t < n5 + n6 + n7; t += T3) {
         if (t < n5) {
-          const int x = t % 6;
+          const int x = 2 * (t % 3);
           int a, b;
-          tri_of(t / 6, a, b);
+          tri_of(t / 3, a, b);
           const int i = k + 2 + a, j = k + 2 + b;
-          row_sub_abt(s.A + 36 * lblk(i, j) + 6 * x, s.A + 36 * lblk(i, k) + 6 * x,
-                      s.A + 36 * lblk(j, k));
+          row2_sub_abt(s.A + 36 * lblk(i, j) + 6 * x, s.A + 36 * lblk(i, k) + 6 * x,
+                       s.A + 36 * lblk(j, k));
         } else if (t < n5 + n6) {
           const int u = t - n5, j = u / 6, c = u % 6;
           float tv[6], zv[6];
@@ -365,6 +390,7 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
     wstamp(st, 2 + k);
   }
   wstamp(st, 40);
+  if (wid == 0) __builtin_amdgcn_s_setprio(0);
   const bool ok = *fail == 0;
   // x = Z^T Z y, then refinement x += Z^T Z (y - S x); v1 = (float) y since the start
   z_mul(s.Z, s.v1, s.v0, N);

@@ -12,7 +12,7 @@
 // MI355X design (DESIGN.md "F-BA for DPVO windows").  A window is
 // latency-bound (~0.5 MB of compulsory traffic per call), so the aim is the
 // shortest dependency chain, not bandwidth:
-//   * ba_plan_kernel (one 1024-thread workgroup, depends on ii/jj/kk only):
+//   * ba_plan_kernel (one 512-thread workgroup, depends on ii/jj/kk only):
 //     groups the edges by patch ONCE (counting sort on kk in LDS, bitonic if
 //     the kk range is too wide; deterministic order inside a patch) and
 //     writes patch offsets + free-pose masks.  Because it reads no pose,
@@ -40,7 +40,7 @@ namespace {
 using namespace bad;
 
 constexpr int kWT = 256;                // iteration kernel threads
-constexpr int kPT = 1024;               // plan kernel threads
+constexpr int kPT = 512;                // plan kernel threads
 constexpr int kWMaxN = 16;
 constexpr int kWMaxE = 4096;
 constexpr int kWMaxG = 256;
@@ -66,6 +66,7 @@ struct Plan {          // written by ba_plan_kernel, read by ba_window_kernel
   int* pkk;            // [E] patch id (kk) of patch u
   int* meta;           // [8] nuniq, fmin, status
   int* status;         // the workspace status word, reset here
+  int* sink;           // caller's sticky status word or null
 };
 
 struct WArgs {
@@ -84,6 +85,7 @@ struct WArgs {
   long long* flags;  // persistent [kFlagWords]
   float* ejg;        // [G][E][12] per relevant edge E entries (fp32), HBM fallback
   int* status;       // [1] OR of status bits (workspace meta)
+  int* sink;         // caller's sticky status word (dpvo_ba_set_status_sink) or null
   int64_t* marks;    // [64] wall-clock stamps of workgroup 0 (may be null)
 };
 
@@ -120,7 +122,7 @@ __device__ __forceinline__ void wg_block(const WArgs& A, int g, int& a, int& b, 
 }
 
 // ===========================================================================
-// plan: group edges by patch (one workgroup, 1024 threads)
+// plan: group edges by patch (one workgroup, 512 threads)
 // ===========================================================================
 __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict__ ii,
                                                       const int64_t* __restrict__ jj,
@@ -132,7 +134,8 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
   int* ctl = (int*)lds;                  // [64]
   int* scr = ctl + 16;                   // scan scratch [>= 17]
   unsigned* code = (unsigned*)(lds + 256);                        // [E] ci | cj << 8
-  char* big = lds + 256 + al16(sizeof(unsigned) * kWMaxE);       // sort area
+  int* kkv = (int*)(lds + 256 + al16(sizeof(unsigned) * kWMaxE)); // [E] kk (clamped)
+  char* big = lds + 256 + 2 * al16(sizeof(unsigned) * kWMaxE);   // sort area
   const int kmaxc = num_patches - 1;
   if (tid == 0) {
     ctl[0] = 0x7fffffff;  // kmin
@@ -150,6 +153,7 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
     }
     kmin = min(kmin, (int)v);
     kmax = max(kmax, (int)v);
+    kkv[e] = (int)v;
     const int64_t gi = ii[e], gj = jj[e];
     const bool fi = gi >= t0 && gi < t0 + N, fj = gj >= t0 && gj < t0 + N;
     const int ci = fi ? (int)(gi - t0) : (int)kFix, cj = fj ? (int)(gj - t0) : (int)kFix;
@@ -175,11 +179,7 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
   const int R = ctl[1] - kmin + 1;
   int* spos = (int*)big;                 // [E] edge at position p
   int* head = spos + kWMaxE;             // [E] head flags -> patch index (scan)
-  auto key_of = [&](int e) -> int {
-    int64_t v = kk[e];
-    v = v < 0 ? 0 : (v > kmaxc ? kmaxc : v);
-    return (int)v - kmin;
-  };
+  auto key_of = [&](int e) -> int { return kkv[e] - kmin; };
   if (R <= kHistMax) {
     int* hist = head + kWMaxE;           // [R]
     for (int v = tid; v < R; v += T) hist[v] = 0;
@@ -270,6 +270,7 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
     plan.meta[0] = nuniq;
     plan.meta[1] = ctl[2];
     plan.meta[2] = ctl[3];
+    if (ctl[3] && plan.sink) atomicOr(plan.sink, ctl[3]);
     *plan.status = 0;  // this call's status word (ORed by the iteration kernel)
   }
 }
@@ -298,7 +299,7 @@ struct WL {  // LDS layout of one workgroup
   char* region;        // union: chunk scratch / reduction table / solver
 };
 
-enum { cNrel = 0, cNrp = 1, cFmin = 2, cFail = 3, cTimeout = 4, cCap = 5, cScan = 16 };
+enum { cNrel = 0, cNrp = 1, cFmin = 2, cFail = 3, cTimeout = 4, cCap = 5, cFailAny = 6, cScan = 16 };
 
 __device__ __forceinline__ unsigned wslot(int gp, int t0, int N, int fmin) {
   if (gp >= t0 && gp < t0 + N) return (unsigned)(gp - t0);
@@ -531,6 +532,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   const int nuniq = A.plan.meta[0], fmin = A.plan.meta[1];
   if (tid == 0) {
     ctl[cFail] = 0;
+    ctl[cFailAny] = 0;
     ctl[cTimeout] = 0;
     ctl[cCap] = 0;
   }
@@ -570,7 +572,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   };
   bool fits = rec0 + rec_bytes(nrel, nrp) + region_b <= (size_t)kWLds;
   if (!fits) {  // contributes nothing; the call reports status 32 (raised by the extension)
-    if (tid == 0) atomicOr(A.status, kStCap);
+    if (tid == 0) ctl[cCap] = 1;
     nrel = nrp = 0;
   }
   size_t o2 = rec0;
@@ -612,7 +614,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     L.roff[ri] = q0;
     rpo[ri] = A.plan.poff[u];
     for (int t = 0; t < ne; t++) L.rp[q0 + t] = (unsigned short)ri;
-    if (ne > kChunk) atomicOr(A.status, kStCap);
+    if (ne > kChunk) ctl[cCap] = 1;
     const int kx = A.plan.pkk[u];
     const float* pk = A.patches + (size_t)kx * 3 * PP;
     const int c11 = P + 1;  // [*][1][1] (ba_cuda.cu:282-285)
@@ -789,7 +791,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     const bool ok = wsolve(sv, N, kRefine, &ctl[cFail]);
     const bool zero = !ok || ctl[cTimeout] != 0;
     for (int k = tid; k < 6 * N; k += kWT) L.dX[k] = zero ? 0.0 : sv.x[k];  // (dpvo/ba.py:17-21)
-    if (!ok && g == 0 && tid == 0) atomicOr(A.status, kStChol);
+    if (!ok && tid == 0) ctl[cFailAny] = 1;
     __syncthreads();
     mark(A, mb + 3);
   }
@@ -851,7 +853,12 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     int st = 0;
     if (ctl[cTimeout]) st |= kStTimeout;
     if (g == 0) st |= A.plan.meta[2];  // kk clamp from the plan
-    if (st) atomicOr(A.status, st);
+    if (ctl[cCap]) st |= kStCap;
+    if (g == 0 && ctl[cFailAny]) st |= kStChol;
+    if (st) {
+      atomicOr(A.status, st);
+      if (A.sink) atomicOr(A.sink, st);
+    }
     if (g == 0) {
       __hip_atomic_store(&A.flags[kEpochWord], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       mark(A, 63);
@@ -917,6 +924,25 @@ long long* wflag_slot(hipStream_t st) {
 }
 }  // namespace
 
+namespace {
+std::mutex g_sink_mu;
+std::map<int, int*> g_sink;  // per device: caller's sticky status word
+int* sink_for_device() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_sink_mu);
+  auto it = g_sink.find(dev);
+  return it == g_sink.end() ? nullptr : it->second;
+}
+}  // namespace
+
+void ba_set_status_sink(int* sink) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_sink_mu);
+  g_sink[dev] = sink;
+}
+
 static Plan plan_view(char* scratch, int E, int* status) {
   Plan p;
   char* s = scratch;
@@ -930,6 +956,7 @@ static Plan plan_view(char* scratch, int E, int* status) {
   s += al256w(sizeof(int) * (size_t)E);
   p.meta = (int*)s;
   p.status = status;
+  p.sink = sink_for_device();
   return p;
 }
 
@@ -1011,6 +1038,7 @@ int ba_window_run(float* poses, float* patches, const float* intrinsics, const f
   a.So = w.So;
   a.G = w.G;
   a.status = status;
+  a.sink = a.plan.sink;
   a.marks = marks;
   hipLaunchKernelGGL(ba_window_kernel, dim3(w.G), dim3(kWT), kWLds, st, a);
   return launch_status();

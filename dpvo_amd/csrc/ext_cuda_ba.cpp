@@ -81,6 +81,7 @@ StatusSlot& slot_for(const torch::Tensor& like) {
     *sl.host = 0;
     TORCH_CHECK(hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) == hipSuccess,
                 "cuda_ba: status event");
+    check_status(dpvo_ba_set_status_sink(sl.acc.data_ptr<int>()), "cuda_ba: status sink");
   }
   return sl;
 }
@@ -99,11 +100,14 @@ void track_status(const torch::Tensor& ws, const torch::Tensor& like, int E, int
   sl.pending = true;
 }
 
+// before a launch: creates the device's slot (registering its status sink, so
+// the window kernels of this very call report into it) and raises a finished
+// earlier call's fatal status
 void poll_status(const torch::Tensor& like) {
   if (is_capturing()) return;
   std::lock_guard<std::mutex> lk(g_st_mu);
-  auto it = g_st.find(like.get_device());
-  if (it != g_st.end()) consume(it->second, false, current_stream());
+  auto& sl = slot_for(like);
+  consume(sl, false, current_stream());
 }
 }  // namespace
 

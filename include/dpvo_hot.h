@@ -224,6 +224,10 @@ int dpvo_ba_forward_planned(float* poses, float* patches, const float* intrinsic
    Graph-capturable (one tiny kernel, no host sync). */
 int dpvo_ba_status_accumulate(const void* workspace, int E, int t0, int t1, int* acc,
                               void* stream);
+/* Register `acc` (device int) as the current device's status sink: the
+   window-path kernels OR their status into it directly (no extra launch per
+   call); dpvo_ba_status_accumulate is then a no-op for that path. */
+int dpvo_ba_set_status_sink(int* acc);
 /* Instrumentation (no reference counterpart): the 128 marks the last
    dpvo_ba_forward on this workspace stamped -- wall clock (100 MHz): [0]
    start, [1] setup, then linearize, patch, schur, solve, update per iteration;
