@@ -228,13 +228,27 @@ def main():
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import cpu_baseline  # baseline infrastructure (CPU port of the reference path)
 
+        # all cores of this process's share of the host (16 on the GPU box;
+        # os.cpu_count() shows the whole machine there), then the 2 threads
+        # DPVO.__init__ sets (dpvo.py:66), then the fork's 1-iteration local BA
         threads = min(16, os.cpu_count() or 1)
-        ips, thr, n = cpu_baseline.measure(G, levels=tuple(levels), budget_s=args.cpu_budget,
-                                           threads=threads, mem=args.mem, C=C)
+        kw = dict(levels=tuple(levels), mem=args.mem, C=C)
+        ips, thr, n = cpu_baseline.measure(G, budget_s=args.cpu_budget, threads=threads,
+                                           iterations=args.ba_iters, **kw)
+        ips2, thr2, n2 = cpu_baseline.measure(G, budget_s=args.cpu_budget, threads=2,
+                                              iterations=args.ba_iters, **kw)
+        ips1, thr1, n1 = cpu_baseline.measure(G, budget_s=0.5 * args.cpu_budget, threads=threads,
+                                              iterations=1, **kw)
         cpu = {"value": ips, "unit": "update-iterations/s", "cores": thr, "kind": "port",
                "sample": f"{n} full {args.config} update iteration(s) (reproject + "
                          f"{len(levels)}-level grid_sample corr + {args.ba_iters} ba.py BA "
-                         f"steps), torch CPU, {thr} threads"}
+                         f"steps), torch CPU, {thr} threads",
+               "os_cpu_count": os.cpu_count(),
+               "two_threads": {"value": ips2, "cores": thr2, "sample": f"{n2} iteration(s)"},
+               "ba_iterations_1": {"value": ips1, "cores": thr1, "sample": f"{n1} iteration(s)"},
+               "calibration": "port == reference corr_torch_forward bit for bit, time ratio "
+                              "0.96-1.01 (profiles/r02_cpu_calibration.json); ba.py port pinned "
+                              "to the reference's fp64 run (tests/test_cpu_baseline.py)"}
 
     if rank == 0:
         out = {

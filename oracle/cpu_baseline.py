@@ -108,8 +108,12 @@ def _exp(xi):
 
 
 # ------------------------------------------------------------------ BA (ba.py)
-def ba_step(poses, patches, intr, target, weight, lmbda, ii, jj, kk, t0, ep=100.0):
-    """One dpvo/ba.py BA call (88-297), dense Schur, B = 1."""
+def ba_step(poses, patches, intr, target, weight, lmbda, ii, jj, kk, t0, ep=100.0, bounds=None):
+    """One dpvo/ba.py BA call (88-297), dense Schur, B = 1.  ``bounds``
+    (xmin, ymin, xmax, ymax) of the projected patch centre (ba.py:165-171);
+    None -> python_ba_wrapper's default [0, 0, W-1, H-1] with W = 2 cx,
+    H = 2 cy (ba.py:355-370).  Works in the dtype of the inputs (the pinning
+    test runs it in float64 against the reference's own fp64 run)."""
     n = int(max(ii.max(), jj.max())) + 1
     fx, fy, cx, cy = intr.unbind(-1)
     X0 = torch.stack([(patches[kk, 0] - cx) / fx, (patches[kk, 1] - cy) / fy,
@@ -132,7 +136,12 @@ def ba_step(poses, patches, intr, target, weight, lmbda, ii, jj, kk, t0, ep=100.
     Gm = torch.cat([Gij[:, :3], torch.ones_like(Gij[:, :1])], -1).unsqueeze(-1)
     Jz = Jp @ Gm
     r = target - coords[:, p // 2, p // 2]
-    v = ((r.norm(dim=-1) < 250) & (Z > 0.2)).float()
+    if bounds is None:
+        bounds = (0.0, 0.0, float(2 * cx) - 1.0, float(2 * cy) - 1.0)
+    cc = coords[:, p // 2, p // 2]
+    inb = (cc[:, 0] > bounds[0]) & (cc[:, 1] > bounds[1]) & (cc[:, 0] < bounds[2]) & \
+        (cc[:, 1] < bounds[3])
+    v = ((r.norm(dim=-1) < 250) & (Z > 0.2) & inb).to(poses.dtype)
     r = (v[:, None] * r).unsqueeze(-1)
     w = (v[:, None] * weight).unsqueeze(-1)
     wJiT, wJjT, wJzT = (w * Ji).transpose(1, 2), (w * Jj).transpose(1, 2), (w * Jz).transpose(1, 2)
@@ -140,9 +149,10 @@ def ba_step(poses, patches, intr, target, weight, lmbda, ii, jj, kk, t0, ep=100.
     iif, jjf = ii - t0, jj - t0
     kx, ku = torch.unique(kk, return_inverse=True, sorted=True)
     m = len(kx)
-    Bm = torch.zeros(nf * nf, 6, 6)
-    Em = torch.zeros(nf * m, 6)
-    vv = torch.zeros(nf, 6)
+    dt = poses.dtype
+    Bm = torch.zeros(nf * nf, 6, 6, dtype=dt)
+    Em = torch.zeros(nf * m, 6, dtype=dt)
+    vv = torch.zeros(nf, 6, dtype=dt)
 
     def add_mat(buf, blocks, a, b, nb):
         ok = (a >= 0) & (b >= 0)
@@ -154,20 +164,21 @@ def ba_step(poses, patches, intr, target, weight, lmbda, ii, jj, kk, t0, ep=100.
     add_mat(Bm, wJjT @ Jj, jjf, jjf, nf)
     add_mat(Em, (wJiT @ Jz).squeeze(-1), iif, ku, m)
     add_mat(Em, (wJjT @ Jz).squeeze(-1), jjf, ku, m)
-    C = torch.zeros(m).index_add_(0, ku, (wJzT @ Jz).view(-1))
+    C = torch.zeros(m, dtype=dt).index_add_(0, ku, (wJzT @ Jz).view(-1))
     okv = iif >= 0
     vv.index_add_(0, iif[okv], (wJiT @ r).squeeze(-1)[okv])
     okv = jjf >= 0
     vv.index_add_(0, jjf[okv], (wJjT @ r).squeeze(-1)[okv])
-    wv = torch.zeros(m).index_add_(0, ku, (wJzT @ r).view(-1))
+    wv = torch.zeros(m, dtype=dt).index_add_(0, ku, (wJzT @ r).view(-1))
     Q = 1.0 / (C + lmbda)
     Bd = Bm.view(nf, nf, 6, 6).permute(0, 2, 1, 3).reshape(6 * nf, 6 * nf)
     Ed = Em.view(nf, m, 6).permute(0, 2, 1).reshape(6 * nf, m)
     S = Bd - (Ed * Q) @ Ed.T
     y = vv.view(-1) - (Ed * Q) @ wv
-    S = S + (ep + 1e-4 * S) * torch.eye(6 * nf)
+    S = S + (ep + 1e-4 * S) * torch.eye(6 * nf, dtype=dt)
     L, info = torch.linalg.cholesky_ex(S)
-    dX = torch.cholesky_solve(y.unsqueeze(-1), L).view(nf, 6) if not info.any() else torch.zeros(nf, 6)
+    dX = (torch.cholesky_solve(y.unsqueeze(-1), L).view(nf, 6) if not info.any()
+          else torch.zeros(nf, 6, dtype=dt))
     dZ = Q * (wv - Ed.T @ dX.view(-1))
     patches = patches.clone()
     patches[kx, 2] = (patches[kx, 2] + dZ.view(-1, 1, 1)).clamp(1e-3, 10.0)
@@ -195,9 +206,11 @@ def update_iteration(state, levels, iterations=2):
     return outs, poses, patches
 
 
-def measure(G, levels=(1, 2, 4, 8), budget_s=15.0, threads=None, mem=None, C=128):
+def measure(G, levels=(1, 2, 4, 8), budget_s=15.0, threads=None, mem=None, C=128, iterations=2):
     """Time update iterations of the CPU port on a bounded sample (>= 1
-    iteration, stop once `budget_s` is spent).  Returns (it/s, threads, n)."""
+    iteration, stop once `budget_s` is spent).  Returns (it/s, threads, n).
+    ``iterations``: BA iterations per update (2 = fastba default; the fork's
+    local call uses 1, dpvo.py:824)."""
     if threads:
         torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
@@ -209,7 +222,7 @@ def measure(G, levels=(1, 2, 4, 8), budget_s=15.0, threads=None, mem=None, C=128
     t0 = time.perf_counter()
     n = 0
     while True:
-        update_iteration(state, levels)
+        update_iteration(state, levels, iterations)
         n += 1
         el = time.perf_counter() - t0
         if el >= budget_s or (n >= 1 and el * (n + 1) / n > 2 * budget_s):
