@@ -540,6 +540,57 @@ torch::Tensor gba_info(torch::Tensor ws, int E, int t0, int t1) {
   return out;
 }
 
+// PatchGraph bookkeeping on the device (dpvo.py:480-568): no host sync.
+static float* opt_f32(const torch::Tensor& t) {
+  return t.defined() && t.numel() ? t.data_ptr<float>() : nullptr;
+}
+
+void pg_append(torch::Tensor ix, torch::Tensor kk_new, torch::Tensor jj_new, torch::Tensor ii,
+               torch::Tensor jj, torch::Tensor kk, torch::Tensor net, torch::Tensor counts) {
+  ix = idx64(ix, "ix");
+  kk_new = idx64(kk_new, "kk");
+  jj_new = idx64(jj_new, "jj");
+  TORCH_CHECK(ii.is_contiguous() && jj.is_contiguous() && kk.is_contiguous() &&
+              counts.is_contiguous() && counts.scalar_type() == torch::kInt32,
+              "pg buffers must be contiguous, counts int32");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ii.device());
+  const int max_edges = ii.numel();
+  const int DIM = net.defined() && net.numel() ? (int)(net.numel() / max_edges) : 0;
+  check_status(dpvo_pg_append(ix.data_ptr<int64_t>(), kk_new.data_ptr<int64_t>(),
+                              jj_new.data_ptr<int64_t>(), kk_new.numel(), ii.data_ptr<int64_t>(),
+                              jj.data_ptr<int64_t>(), kk.data_ptr<int64_t>(), opt_f32(net), DIM,
+                              counts.data_ptr<int>(), max_edges, current_stream()),
+               "cuda_ba.pg_append");
+}
+
+void pg_remove(c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> ix, int64_t thresh,
+               int64_t lc_min, bool store, std::vector<torch::Tensor> act,
+               std::vector<torch::Tensor> back, std::vector<torch::Tensor> inac,
+               torch::Tensor counts, torch::Tensor pos) {
+  TORCH_CHECK(act.size() == 6 && back.size() == 6 && inac.size() == 5,
+              "act/back: [ii, jj, kk, net, weight, target]; inac: [ii, jj, kk, weight, target]");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(counts.device());
+  const int max_edges = act[0].numel();
+  const int DIM = act[3].defined() && act[3].numel() ? (int)(act[3].numel() / max_edges) : 0;
+  const uint8_t* mp = nullptr;
+  torch::Tensor m8;
+  if (mask && mask->defined()) {
+    m8 = mask->to(torch::kUInt8).contiguous();
+    check_device(m8, "mask");
+    mp = m8.data_ptr<uint8_t>();
+  }
+  const int64_t* ixp = (ix && ix->defined()) ? idx64(*ix, "ix").data_ptr<int64_t>() : nullptr;
+  auto L = [](const torch::Tensor& t) { return t.data_ptr<int64_t>(); };
+  check_status(dpvo_pg_remove(mp, ixp, thresh, lc_min, store ? 1 : 0, L(act[0]), L(act[1]),
+                              L(act[2]), opt_f32(act[3]), act[4].data_ptr<float>(),
+                              act[5].data_ptr<float>(), L(back[0]), L(back[1]), L(back[2]),
+                              opt_f32(back[3]), back[4].data_ptr<float>(), back[5].data_ptr<float>(),
+                              L(inac[0]), L(inac[1]), L(inac[2]), inac[3].data_ptr<float>(),
+                              inac[4].data_ptr<float>(), DIM, counts.data_ptr<int>(),
+                              pos.data_ptr<int>(), max_edges, current_stream()),
+               "cuda_ba.pg_remove");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("forward", &ba_forward, "BA forward operator");
   m.def("neighbors", &ba_neighbors, "temporal neighboor indicies");
@@ -551,6 +602,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("solve_update", &ba_solve_update, "Cholesky solve + pose/patch retraction");
   m.def("last_status", &ba_last_status, "status word of the last BA on a workspace");
   m.def("max_free_poses", &dpvo_ba_max_free_poses);
+  m.def("pg_append", &pg_append, "PatchGraph.append_factors on the device (dpvo.py:480-521)");
+  m.def("pg_remove", &pg_remove, "PatchGraph.remove_factors on the device (dpvo.py:523-568)");
   m.def("plan_supported", &ba_plan_supported, "window path available for (E, t0, t1, P)");
   m.def("plan", &ba_plan, "group the edges by patch (reads ii/jj/kk only) -> workspace");
   m.def("forward_planned", &ba_forward_planned, "BA iterations on a planned workspace");

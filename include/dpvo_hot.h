@@ -322,6 +322,31 @@ int dpvo_lie_forward(int group, int op, int dtype, int n, const void* X, const v
 int dpvo_lie_backward(int group, int op, int dtype, int n, const void* grad, const void* X,
                       const void* Y, void* out0, void* out1, void* stream);
 
+/* PatchGraph edge bookkeeping on the device (dpvo/dpvo.py:480-568,
+   dpvo/patchgraph.py:11-63), static MAX_EDGES buffers, counts in the device
+   int array `counts`: [0] num_edges, [1] num_edges_inac, [2] error flags
+   (1 append overflow -> edges not added; 2 inactive store full -> removed
+   edges not stored, like the reference's warning), [3..4] scratch.  No host
+   synchronisation.
+   dpvo_pg_append replaces append_factors(ii=kk_new, jj=jj_new): edges at
+   [num, num + n), ii = ix[kk], net rows zeroed (net may be null).
+   dpvo_pg_remove replaces remove_factors(mask, store): mask (uint8, 1 =
+   remove, length >= num) or, when mask is null, the DPVO window rule
+   ix[kk] < thresh (dpvo.py:684) sparing loop-closure edges with
+   jj - ii > 30 and jj > lc_min when lc_min >= 0 (:685-688).  Kept edges are
+   compacted in order into the *_b ("back") buffers -- the caller swaps
+   them with the active set -- and removed ones appended in order to the
+   inactive store when `store`.  pos: int scratch [max_edges]. */
+int dpvo_pg_append(const int64_t* ix, const int64_t* kk_new, const int64_t* jj_new, int n,
+                   int64_t* ii, int64_t* jj, int64_t* kk, float* net, int DIM, int* counts,
+                   int max_edges, void* stream);
+int dpvo_pg_remove(const uint8_t* mask, const int64_t* ix, int64_t thresh, int64_t lc_min,
+                   int store, int64_t* ii, int64_t* jj, int64_t* kk, float* net, float* weight,
+                   float* target, int64_t* ii_b, int64_t* jj_b, int64_t* kk_b, float* net_b,
+                   float* weight_b, float* target_b, int64_t* ii_i, int64_t* jj_i, int64_t* kk_i,
+                   float* weight_i, float* target_i, int DIM, int* counts, int* pos,
+                   int max_edges, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
