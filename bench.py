@@ -181,6 +181,9 @@ def main():
     ap.add_argument("--sharded", action="store_true",
                     help="cfg4 global BA, edge-sharded over the ranks (one RCCL all_reduce of "
                          "the packed (S, y) per iteration); --config picks the large graph")
+    ap.add_argument("--features", choices=["f32", "f16"], default="f32",
+                    help="feature dtype of the pyramid / gmap rings (f16 = the fork's "
+                         "MIXED_PRECISION runtime: A-CORR on v_mfma_f32_16x16x16_f16)")
     ap.add_argument("--eager", action="store_true",
                     help="launch every kernel from Python each step (default: replay the "
                          "step as one captured hipGraph)")
@@ -210,11 +213,13 @@ def main():
     # (corr_nhwc.hip).  Every step inserts one frame (NCHW level 1 -> pooled,
     # channels-last levels, one launch) so the per-frame cost of the pyramid and
     # its layout is inside the timed region.
+    fdt = torch.float16 if args.features == "f16" else torch.float32
+    feat_bytes = 2 if args.features == "f16" else 4
     pyr_nchw = synthetic.make_features(mem=args.mem, C=C, levels=levels, seed=args.seed,
-                                       device=dev)
+                                       device=dev, dtype=fdt)
     pyr = [synthetic.channels_last(p) for p in pyr_nchw]
     # gmap: patch features of every (frame, slot), DPVO's pmem = mem ring
-    gbuf = torch.zeros(1, args.mem * G.M, C, P, P, device=dev)
+    gbuf = torch.zeros(1, args.mem * G.M, C, P, P, device=dev, dtype=fdt)
     centres = D.patches[: G.F * G.M, :2, P // 2, P // 2]  # [F*M, 2] (x, y)
     for f in range(G.F):
         gbuf[0, f * G.M:(f + 1) * G.M] = altcorr.patchify(
@@ -270,7 +275,8 @@ def main():
     corr_ms = sorted(a.elapsed_time(b) for a, b in evs)[n_ev // 2]
     coords0 = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk)
     alg_bytes, per_level = algorithmic_corr_bytes(
-        coords0, [f.shape[3] for f in pyr], [f.shape[4] for f in pyr], scales, C, P, 3, 4)
+        coords0, [f.shape[3] for f in pyr], [f.shape[4] for f in pyr], scales, C, P, 3,
+        feat_bytes)
 
     graph = None
     if not args.eager:
@@ -355,13 +361,15 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if args.features == "f32" else "f16 features, f32 accumulate",
             "data": "synthetic (SURVEY 8d cfg2 recipe, seeded)",
             "launch": "eager" if graph is None else "hipGraph replay of one captured step",
             "ba_plan": "inline" if args.no_overlap else "side stream, concurrent with A-CORR",
             "config": {
                 "workload": f"{args.config}: {G.M} patches/frame x {G.E} edges, p={P}, "
-                            f"{len(levels)}-level pyramid {levels}, fp32, BA {args.ba_iters} iters",
+                            f"{len(levels)}-level pyramid {levels}, "
+                            f"{'fp32' if args.features == 'f32' else 'fp16'} features, "
+                            f"BA {args.ba_iters} iters",
                 "patches_per_frame": G.M, "edges": G.E, "frames": G.F, "levels": levels,
                 "radius": 3, "channels": C, "feature_ring": args.mem,
                 "parallelism": f"replicas x{world}",
@@ -373,7 +381,7 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": pmc_traffic(args.config),
+                "traffic": pmc_traffic(args.config) if args.features == "f32" else None,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "kernel_ms": corr_ms,
                 "per_level": per_level,

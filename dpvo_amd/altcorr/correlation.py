@@ -120,6 +120,8 @@ def corr_levels(fmap1, pyramid, coords, ii, jj, radius=3, scales=(1, 4), order=N
 
     Levels stored channels-last (``synthetic.channels_last`` / ``to_channels_last``)
     take the matrix-core path (corr_nhwc.hip); NCHW levels the VALU path.
+    float16 features (the fork's MIXED_PRECISION runtime) run on
+    v_mfma_f32_16x16x16_f16 with fp32 accumulation; the output stays float32.
     ``order`` (int32 [E], from ``fastba.reproject(..., mem=N2)``): process
     edges grouped by target frame, one group range per XCD (same results)."""
     require_gpu(fmap1)

@@ -17,6 +17,8 @@
 // consecutive K steps), D = G tile -> LDS.  One wave per edge handles every
 // level; the bilinear + permute of all levels is kept in registers and
 // stored once per edge as contiguous [.., L] float4 rows.
+#include <type_traits>
+
 #include "common.hpp"
 
 // diagnostic builds (scripts/micro/corr_bench.hip) define CORR_STAMP(slot) to
@@ -38,7 +40,7 @@ constexpr int kOutPerLane = 8;  // (2R+1)^2 * p*p <= 512 outputs per level
 constexpr int kNpMax = 16;      // p*p <= 16 (one MFMA row tile)
 
 struct NhwcLevels {
-  const float* f2[kMaxL];
+  const void* f2[kMaxL];  // float or __half, [B, N2, H, W, C]
   int H2[kMaxL], W2[kMaxL];
   float scale[kMaxL];
 };
@@ -50,6 +52,37 @@ struct NhwcGeom {
 };
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+// fp16 features (DPVO's MIXED_PRECISION runtime, correlation_kernel.py:552-654):
+// v_mfma_f32_16x16x16_f16, fp32 accumulation (documented deviation: the
+// reference accumulates fp16 products in fp16).  K order: lane group q
+// (= lane >> 4) owns channels [32q, 32q + 32); K step h uses its channels
+// 32q + 4h .. + 3 for both A (gmap patch) and B (box pixels), so a lane's
+// B data of a tile is ONE contiguous 64-B run of its pixel (4 x 16-B loads).
+template <typename T>
+struct CorrT;
+template <>
+struct CorrT<float> {
+  static constexpr int kVecs = 8;  // 16-B loads per lane per tile (128 B)
+  static constexpr int kLaneCh = 4;  // channel offset of lane group q: 4 q (+ 16 h)
+};
+template <>
+struct CorrT<__half> {
+  static constexpr int kVecs = 4;  // 4 x 16 B = 32 halves per lane per tile
+  static constexpr int kLaneCh = 32;
+};
+
+__device__ __forceinline__ f16x4 h4_lo(const uint4& v) {
+  f16x4 r;
+  __builtin_memcpy(&r, &v.x, 8);
+  return r;
+}
+__device__ __forceinline__ f16x4 h4_hi(const uint4& v) {
+  f16x4 r;
+  __builtin_memcpy(&r, &v.z, 8);
+  return r;
+}
 
 // One wave per edge, every level (the gmap patch and the coordinates are
 // loaded once per edge).  The kernel is latency-bound: at DPVO sizes there
@@ -65,8 +98,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 //  * a level's bilinear + permute runs as soon as its last tile is in LDS,
 //    from per-lane output codes computed once (no integer division per level).
 
+template <typename T>
 __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 waves) per CU: every edge resident at once
-    corr_nhwc_kernel(const float* __restrict__ fmap1, NhwcLevels lv, int L,
+    corr_nhwc_kernel(const T* __restrict__ fmap1, NhwcLevels lv, int L,
                      const float* __restrict__ coords, const int64_t* __restrict__ ii,
                      const int64_t* __restrict__ jj, int B, int M, int np, int N1, int N2, int R,
                      const int* __restrict__ order, float* __restrict__ out) {
@@ -102,28 +136,43 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   // fragments: lane (i = lane & 15, q = lane >> 4) holds f1[c][i] for
   // c = 16h + 4q + s at K step 4h + s (the same channel order as the B loads)
   const int ai = lane & 15, aq = lane >> 4;
-  float Af[kNhwcC / 4];
+  constexpr bool kHalf = std::is_same<T, __half>::value;
+  float Af[kHalf ? 1 : kNhwcC / 4];
+  f16x4 Afh[kHalf ? kNhwcC / 16 : 1];
   {
-    const float* f1 = fmap1 + ((size_t)b * N1 + (idx_ok ? ix : 0)) * C * np;
-    const int n4 = (C * np) >> 2;  // C * np is a multiple of 4 (C = 128)
-    float4 st[(kNhwcC * kNpMax / 4 + kWave - 1) / kWave];
+    // 16-B units of the [C][np] patch (4 floats or 8 halves each)
+    constexpr int kPer = 16 / sizeof(T);
+    const T* f1 = fmap1 + ((size_t)b * N1 + (idx_ok ? ix : 0)) * C * np;
+    const int n16 = (C * np) / kPer;  // C * np is a multiple of 8 (C = 128)
+    constexpr int kR = (kNhwcC * kNpMax / kPer + kWave - 1) / kWave;
+    uint4 st[kR];
 #pragma unroll
-    for (int r = 0; r < (kNhwcC * kNpMax / 4 + kWave - 1) / kWave; r++) {
+    for (int r = 0; r < kR; r++) {
       const int v = lane + kWave * r;
-      st[r] = (v < n4) ? reinterpret_cast<const float4*>(f1)[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+      st[r] = (v < n16) ? reinterpret_cast<const uint4*>(f1)[v] : make_uint4(0u, 0u, 0u, 0u);
     }
 #pragma unroll
-    for (int r = 0; r < (kNhwcC * kNpMax / 4 + kWave - 1) / kWave; r++) {
+    for (int r = 0; r < kR; r++) {
       const int v = lane + kWave * r;
-      if (v < n4) reinterpret_cast<float4*>(G)[v] = st[r];
+      if (v < n16) reinterpret_cast<uint4*>(G)[v] = st[r];
     }
     wave_lds_sync();
     const bool arow = idx_ok && ai < np;
+    if constexpr (kHalf) {
+      const __half* Gh = reinterpret_cast<const __half*>(G);
 #pragma unroll
-    for (int h = 0; h < kNhwcC / 16; h++)
+      for (int h = 0; h < kNhwcC / 16; h++)
 #pragma unroll
-      for (int s = 0; s < 4; s++)
-        Af[4 * h + s] = arow ? G[(16 * h + 4 * aq + s) * np + ai] : 0.0f;
+        for (int s = 0; s < 4; s++)
+          Afh[h][s] = arow ? (_Float16)__half2float(Gh[(32 * aq + 4 * h + s) * np + ai])
+                           : (_Float16)0.0f;
+    } else {
+#pragma unroll
+      for (int h = 0; h < kNhwcC / 16; h++)
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+          Af[4 * h + s] = arow ? G[(16 * h + 4 * aq + s) * np + ai] : 0.0f;
+    }
   }
 
   // ---- geometry of every level up front, lane-parallel: lane (l = lane >> 4,
@@ -251,15 +300,15 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     const int nt = wave_uniform(geo[l].ntile);
     if (nt > kMaxTiles) {  // raw[k][yy][xx] directly into G
       const int H2 = lv.H2[l], W2 = lv.W2[l];
-      const float* f2 = lv.f2[l] + ((size_t)b * N2 + jx) * H2 * W2 * C;
+      const T* f2 = static_cast<const T*>(lv.f2[l]) + ((size_t)b * N2 + jx) * H2 * W2 * C;
       for (int e = lane; e < np * D * D; e += kWave) {
         const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
         const int i1 = geo[l].y0[k] + yy - R, j1 = geo[l].x0[k] + xx - R;
         float sacc = 0.f;
         if (idx_ok && i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
-          const float* px = f2 + ((size_t)i1 * W2 + j1) * C;
-          const float* f1 = fmap1 + ((size_t)b * N1 + ix) * C * np;
-          for (int c = 0; c < C; c++) sacc += f1[(size_t)c * np + k] * px[c];
+          const T* px = f2 + ((size_t)i1 * W2 + j1) * C;
+          const T* f1 = fmap1 + ((size_t)b * N1 + ix) * C * np;
+          for (int c = 0; c < C; c++) sacc += to_acc(f1[(size_t)c * np + k]) * to_acc(px[c]);
         }
         G[e] = sacc;
       }
@@ -272,9 +321,9 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   }
 
   // ---- flattened fast-path tiles, kRing - 1 in flight
-  const int T = cum[L];
-  auto tile_src = [&](int i) -> const float* {
-    i = min(i, max(T - 1, 0));  // past the end: re-read the last tile (never used)
+  const int nT = cum[L];
+  auto tile_src = [&](int i) -> const T* {
+    i = min(i, max(nT - 1, 0));  // past the end: re-read the last tile (never used)
     const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
     const int t = i - (j == 0 ? 0 : j == 1 ? cum[1] : j == 2 ? cum[2] : cum[3]);
     const int l = level_at(j);
@@ -284,50 +333,66 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     const int px = min(16 * t + ai, max(npx - 1, 0));  // pad columns read pixel npx-1
     const int r = (int)(((float)px + 0.5f) * rbw), cc = px - r * max(bw0, 1);
     const int H2 = lv.H2[l], W2 = lv.W2[l];
-    const float* f2 = lv.f2[l] + ((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 * C;
+    const T* f2 = static_cast<const T*>(lv.f2[l]) + ((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 * C;
     return f2 + ((size_t)(wave_uniform(gg->ylo) + r) * W2 + wave_uniform(gg->xlo) + cc) * C +
-           4 * aq;
+           CorrT<T>::kLaneCh * aq;
   };
-  if (T > 0) {
+  // 16-B vector v of a lane's tile data: fp32 +16 h floats apart, fp16 contiguous
+  auto tile_vec = [&](const T* s, int h) -> uint4 {
+    return *reinterpret_cast<const uint4*>(s + (kHalf ? 8 * h : 16 * h));
+  };
+  if (nT > 0) {
     // register ring: cur = tile i, n1 / n2 = tiles i + 1, i + 2 in flight;
     // one loop body (rotation by register moves, which issue in the MFMA
     // shadow) keeps the kernel small enough for the instruction cache
-    float4 cur[8], n1[8], n2[8];
+    constexpr int V = CorrT<T>::kVecs;
+    uint4 cur[V], n1[V], n2[V];
     {
-      const float* s0 = tile_src(0);
-      const float* s1 = tile_src(1);
-      const float* s2 = tile_src(2);
+      const T* s0 = tile_src(0);
+      const T* s1 = tile_src(1);
+      const T* s2 = tile_src(2);
 #pragma unroll
-      for (int h = 0; h < 8; h++) cur[h] = *reinterpret_cast<const float4*>(s0 + 16 * h);
+      for (int h = 0; h < V; h++) cur[h] = tile_vec(s0, h);
 #pragma unroll
-      for (int h = 0; h < 8; h++) n1[h] = *reinterpret_cast<const float4*>(s1 + 16 * h);
+      for (int h = 0; h < V; h++) n1[h] = tile_vec(s1, h);
 #pragma unroll
-      for (int h = 0; h < 8; h++) n2[h] = *reinterpret_cast<const float4*>(s2 + 16 * h);
+      for (int h = 0; h < V; h++) n2[h] = tile_vec(s2, h);
     }
-    for (int i = 0; i < T; i++) {
+    for (int i = 0; i < nT; i++) {
       // two accumulators (even / odd channel groups): two independent MFMA
       // chains, summed once per tile in a fixed order
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (kHalf) {
+        // 8 K steps of 16 channels: vector h holds steps 2h (lo) and 2h + 1 (hi)
 #pragma unroll
-      for (int h = 0; h < 8; h += 2) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 0], cur[h].x, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 4], cur[h + 1].x, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 1], cur[h].y, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 5], cur[h + 1].y, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 2], cur[h].z, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 6], cur[h + 1].z, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 3], cur[h].w, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 7], cur[h + 1].w, acc1, 0, 0, 0);
+        for (int h = 0; h < V; h++) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x16f16(Afh[2 * h], h4_lo(cur[h]), acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x16f16(Afh[2 * h + 1], h4_hi(cur[h]), acc1, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < 8; h += 2) {
+          const float4 c0 = __builtin_bit_cast(float4, cur[h]);
+          const float4 c1 = __builtin_bit_cast(float4, cur[h + 1]);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 0], c0.x, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 4], c1.x, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 1], c0.y, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 5], c1.y, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 2], c0.z, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 6], c1.z, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 3], c0.w, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 7], c1.w, acc1, 0, 0, 0);
+        }
       }
 #pragma unroll
-      for (int h = 0; h < 8; h++) {
+      for (int h = 0; h < V; h++) {
         cur[h] = n1[h];
         n1[h] = n2[h];
       }
       {  // tile i + 3 (past the end: the last tile again, never used)
-        const float* src = tile_src(i + 3);
+        const T* src = tile_src(i + 3);
 #pragma unroll
-        for (int h = 0; h < 8; h++) n2[h] = *reinterpret_cast<const float4*>(src + 16 * h);
+        for (int h = 0; h < V; h++) n2[h] = tile_vec(src, h);
       }
       const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
       const int lb = (j == 0 ? 0 : j == 1 ? cum[1] : j == 2 ? cum[2] : cum[3]);
@@ -407,25 +472,50 @@ constexpr int kInsTY = 8, kInsTX = 32, kInsTC = 32;
 constexpr int kInsCS = kInsTY * kInsTX + 1;  // channel stride (+1: no bank conflicts)
 
 struct InsLevels {
-  float* dst[kMaxL];
+  void* dst[kMaxL];  // float or __half (the source's dtype)
   int s[kMaxL];
 };
 
 // level-1 copy of the LDS tile: one float4 (4 channels) per lane, 8 lanes per
 // pixel = one 128-B run of the channels-last row
-__device__ __forceinline__ void ins_copy(const float* tile, float* dstl, int tx0, int ty0,
+// fp16 pyramids (MIXED_PRECISION): the tile holds the exact fp32 values of
+// the halves, pools accumulate in fp32 and round once (torch's avg_pool2d
+// accscalar_t path), copies are exact
+__device__ __forceinline__ void st4(float* d, float a, float b, float c, float e) {
+  *reinterpret_cast<float4*>(d) = make_float4(a, b, c, e);
+}
+__device__ __forceinline__ void st4(__half* d, float a, float b, float c, float e) {
+  __half2 lo = __floats2half2_rn(a, b), hi = __floats2half2_rn(c, e);
+  uint2 u;
+  __builtin_memcpy(&u.x, &lo, 4);
+  __builtin_memcpy(&u.y, &hi, 4);
+  *reinterpret_cast<uint2*>(d) = u;
+}
+__device__ __forceinline__ void st1(float* d, float v) { *d = v; }
+__device__ __forceinline__ void st1(__half* d, float v) { *d = __float2half_rn(v); }
+__device__ __forceinline__ float4 ld4(const float* s) { return *reinterpret_cast<const float4*>(s); }
+__device__ __forceinline__ float4 ld4(const __half* s) {
+  const uint2 u = *reinterpret_cast<const uint2*>(s);
+  __half2 lo, hi;
+  __builtin_memcpy(&lo, &u.x, 4);
+  __builtin_memcpy(&hi, &u.y, 4);
+  const float2 a = __half22float2(lo), b = __half22float2(hi);
+  return make_float4(a.x, a.y, b.x, b.y);
+}
+
+template <typename T>
+__device__ __forceinline__ void ins_copy(const float* tile, T* dstl, int tx0, int ty0,
                                          int c0, int C, int H, int W, int tid) {
   for (int it = tid; it < kInsTY * kInsTX * 8; it += 256) {
     const int cg = it & 7, q = it >> 3, py = q / kInsTX, px = q % kInsTX;
     const int oy = ty0 + py, ox = tx0 + px, gc = c0 + 4 * cg;
     if (oy >= H || ox >= W || gc >= C) continue;
     const float* t = tile + (4 * cg) * kInsCS + py * kInsTX + px;
-    float* dst = dstl + ((size_t)oy * W + ox) * C + gc;
+    T* dst = dstl + ((size_t)oy * W + ox) * C + gc;
     if (gc + 4 <= C && (C & 3) == 0) {
-      *reinterpret_cast<float4*>(dst) =
-          make_float4(t[0], t[kInsCS], t[2 * kInsCS], t[3 * kInsCS]);
+      st4(dst, t[0], t[kInsCS], t[2 * kInsCS], t[3 * kInsCS]);
     } else {
-      for (int k = 0; k < 4 && gc + k < C; k++) dst[k] = t[k * kInsCS];
+      for (int k = 0; k < 4 && gc + k < C; k++) st1(dst + k, t[k * kInsCS]);
     }
   }
 }
@@ -434,8 +524,8 @@ __device__ __forceinline__ void ins_copy(const float* tile, float* dstl, int tx0
 // lanes per pixel (a 128-B run); the S*S window is summed in avg_pool2d's
 // row-major order and divided by S^2, fully unrolled so the LDS reads issue
 // back to back (bit-exact with torch)
-template <int S>
-__device__ __forceinline__ void ins_pool(const float* tile, float* dstl, int tx0, int ty0,
+template <int S, typename T>
+__device__ __forceinline__ void ins_pool(const float* tile, T* dstl, int tx0, int ty0,
                                          int c0, int C, int H, int W, int tid) {
   constexpr int nty = kInsTY / S, ntx = kInsTX / S;
   const int Hs = H / S, Ws = W / S, oy0 = ty0 / S, ox0 = tx0 / S;
@@ -452,17 +542,18 @@ __device__ __forceinline__ void ins_pool(const float* tile, float* dstl, int tx0
     float acc = 0.0f;
 #pragma unroll
     for (int k = 0; k < S * S; k++) acc += w[k];
-    dstl[((size_t)oy * Ws + ox) * C + gc] = acc / (float)(S * S);
+    st1(dstl + ((size_t)oy * Ws + ox) * C + gc, acc / (float)(S * S));
   }
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256)
-    pyramid_insert_kernel(const float* __restrict__ src, InsLevels lv, int L, int C, int H,
+    pyramid_insert_kernel(const T* __restrict__ src, InsLevels lv, int L, int C, int H,
                           int W) {
   __shared__ float tile[kInsTC * kInsCS];
   const int tx0 = blockIdx.x * kInsTX, ty0 = blockIdx.y * kInsTY, c0 = blockIdx.z * kInsTC;
   const int tid = threadIdx.x;
-  // load: 32 channels x 8 rows x 32 px as float4 (8 per thread, all issued
+  // load: 32 channels x 8 rows x 32 px, 4 px per load (8 per thread, all issued
   // before the first LDS store: one HBM latency per tile, not eight)
   if ((W & 3) == 0) {
     float4 v[8];
@@ -471,9 +562,8 @@ __global__ void __launch_bounds__(256)
       const int k = tid + 256 * r;  // (c, y, x4) = (k >> 6, (k >> 3) & 7, k & 7)
       const int c = k >> 6, y = (k >> 3) & 7, x = 4 * (k & 7);
       const int gx = tx0 + x, gy = ty0 + y, gc = c0 + c;
-      v[r] = (gx < W && gy < H && gc < C)
-                 ? *reinterpret_cast<const float4*>(src + ((size_t)gc * H + gy) * W + gx)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[r] = (gx < W && gy < H && gc < C) ? ld4(src + ((size_t)gc * H + gy) * W + gx)
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int r = 0; r < 8; r++) {
@@ -492,7 +582,7 @@ __global__ void __launch_bounds__(256)
       const int k = tid + 256 * r;
       const int x = k & 31, y = (k >> 5) & 7, c = k >> 8;
       const int gx = tx0 + x, gy = ty0 + y, gc = c0 + c;
-      v[r] = (gx < W && gy < H && gc < C) ? src[((size_t)gc * H + gy) * W + gx] : 0.0f;
+      v[r] = (gx < W && gy < H && gc < C) ? to_acc(src[((size_t)gc * H + gy) * W + gx]) : 0.0f;
     }
 #pragma unroll
     for (int r = 0; r < 32; r++) {
@@ -503,11 +593,12 @@ __global__ void __launch_bounds__(256)
   __syncthreads();
   // level 1: one float4 (4 channels) per lane, 8 lanes per pixel = one 128-B run
   for (int l = 0; l < L; l++) {
+    T* d = static_cast<T*>(lv.dst[l]);
     switch (lv.s[l]) {
-      case 1: ins_copy(tile, lv.dst[l], tx0, ty0, c0, C, H, W, tid); break;
-      case 2: ins_pool<2>(tile, lv.dst[l], tx0, ty0, c0, C, H, W, tid); break;
-      case 4: ins_pool<4>(tile, lv.dst[l], tx0, ty0, c0, C, H, W, tid); break;
-      default: ins_pool<8>(tile, lv.dst[l], tx0, ty0, c0, C, H, W, tid); break;
+      case 1: ins_copy(tile, d, tx0, ty0, c0, C, H, W, tid); break;
+      case 2: ins_pool<2>(tile, d, tx0, ty0, c0, C, H, W, tid); break;
+      case 4: ins_pool<4>(tile, d, tx0, ty0, c0, C, H, W, tid); break;
+      default: ins_pool<8>(tile, d, tx0, ty0, c0, C, H, W, tid); break;
     }
   }
 }
@@ -522,7 +613,7 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
     int M, int C, int H, int W, int N1, int N2, int radius, int dtype, float* out, void* stream) {
   if (L <= 0 || radius < 0 || radius > 7 || C <= 0 || H <= 0 || W <= 0) return DPVO_ERR_INVALID;
   const int np = H * W, Dp = 2 * radius + 1;
-  if (dtype != DPVO_F32 || C != kNhwcC || L > kMaxL || np > kNpMax ||
+  if ((dtype != DPVO_F32 && dtype != DPVO_F16) || C != kNhwcC || L > kMaxL || np > kNpMax ||
       Dp * Dp * np > kOutPerLane * kWave)
     return DPVO_ERR_UNSUPPORTED;
   if (B * M == 0) return DPVO_OK;
@@ -530,7 +621,7 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   NhwcLevels lv = {};
   for (int l = 0; l < L; l++) {
     if (!fmap2[l] || H2[l] <= 0 || W2[l] <= 0 || !(scale[l] > 0.f)) return DPVO_ERR_INVALID;
-    lv.f2[l] = (const float*)fmap2[l];
+    lv.f2[l] = fmap2[l];
     lv.H2[l] = H2[l];
     lv.W2[l] = W2[l];
     lv.scale[l] = scale[l];
@@ -545,9 +636,15 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   unsigned grid = (unsigned)((units + kNhwcWaves - 1) / kNhwcWaves);
   const bool ordered = order && B == 1;
   if (ordered) grid = 8u * (unsigned)((grid + 7) / 8);
-  hipLaunchKernelGGL(corr_nhwc_kernel, dim3(grid), dim3(kNhwcWaves * kWave), smem,
-                     as_stream(stream), (const float*)fmap1, lv, L, coords, ii, jj, B, M, np, N1,
-                     N2, radius, ordered ? (const int*)order : (const int*)nullptr, out);
+  const int* ord = ordered ? (const int*)order : (const int*)nullptr;
+  if (dtype == DPVO_F16)
+    hipLaunchKernelGGL(corr_nhwc_kernel<__half>, dim3(grid), dim3(kNhwcWaves * kWave), smem,
+                       as_stream(stream), (const __half*)fmap1, lv, L, coords, ii, jj, B, M, np,
+                       N1, N2, radius, ord, out);
+  else
+    hipLaunchKernelGGL(corr_nhwc_kernel<float>, dim3(grid), dim3(kNhwcWaves * kWave), smem,
+                       as_stream(stream), (const float*)fmap1, lv, L, coords, ii, jj, B, M, np,
+                       N1, N2, radius, ord, out);
   return launch_status();
 }
 
@@ -585,17 +682,21 @@ DPVO_EXPORT int dpvo_feature_to_nhwc(const void* src, void* dst, int count, int 
 DPVO_EXPORT int dpvo_feature_pyramid_insert(const void* src, void* const* dst, const int* scale,
                                             int L, int C, int H, int W, int dtype, void* stream) {
   if (!src || !dst || !scale || L <= 0 || C <= 0 || H <= 0 || W <= 0) return DPVO_ERR_INVALID;
-  if (dtype != DPVO_F32 || L > kMaxL) return DPVO_ERR_UNSUPPORTED;
+  if ((dtype != DPVO_F32 && dtype != DPVO_F16) || L > kMaxL) return DPVO_ERR_UNSUPPORTED;
   InsLevels lv = {};
   for (int l = 0; l < L; l++) {
     const int s = scale[l];
     if (!dst[l]) return DPVO_ERR_INVALID;
     if (s != 1 && s != 2 && s != 4 && s != 8) return DPVO_ERR_UNSUPPORTED;
-    lv.dst[l] = (float*)dst[l];
+    lv.dst[l] = dst[l];
     lv.s[l] = s;
   }
   const dim3 grid((W + kInsTX - 1) / kInsTX, (H + kInsTY - 1) / kInsTY, (C + kInsTC - 1) / kInsTC);
-  hipLaunchKernelGGL(pyramid_insert_kernel, grid, dim3(256), 0, as_stream(stream),
-                     (const float*)src, lv, L, C, H, W);
+  if (dtype == DPVO_F16)
+    hipLaunchKernelGGL(pyramid_insert_kernel<__half>, grid, dim3(256), 0, as_stream(stream),
+                       (const __half*)src, lv, L, C, H, W);
+  else
+    hipLaunchKernelGGL(pyramid_insert_kernel<float>, grid, dim3(256), 0, as_stream(stream),
+                       (const float*)src, lv, L, C, H, W);
   return launch_status();
 }

@@ -68,7 +68,8 @@ void feature_pyramid_insert(torch::Tensor src, std::vector<torch::Tensor> dst,
   check_device(src, "src");
   TORCH_CHECK(src.dim() == 3, "src must be [C, H, W]");
   TORCH_CHECK(dst.size() == scales.size() && !dst.empty(), "one scale per destination level");
-  TORCH_CHECK(src.scalar_type() == torch::kFloat32, "src must be float32");
+  TORCH_CHECK(src.scalar_type() == torch::kFloat32 || src.scalar_type() == torch::kFloat16,
+              "src must be float32 or float16");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(src.device());
   src = src.contiguous();
   const int C = src.size(0), H = src.size(1), W = src.size(2);
@@ -78,16 +79,17 @@ void feature_pyramid_insert(torch::Tensor src, std::vector<torch::Tensor> dst,
     const torch::Tensor& d = dst[l];
     check_device(d, "dst");
     const int s = (int)scales[l];
-    TORCH_CHECK(d.scalar_type() == torch::kFloat32 && d.dim() == 3 && d.size(0) == C &&
+    TORCH_CHECK(d.scalar_type() == src.scalar_type() && d.dim() == 3 && d.size(0) == C &&
                     s > 0 && d.size(1) == H / s && d.size(2) == W / s,
-                "dst level ", l, " must be float32 [C, H/s, W/s]");
+                "dst level ", l, " must be [C, H/s, W/s] of src's dtype");
     TORCH_CHECK(d.stride(0) == 1 && d.stride(2) == C && d.stride(1) == (int64_t)C * d.size(2),
                 "dst level ", l, " must be channels-last");
     ptrs.push_back(d.data_ptr());
     sc.push_back(s);
   }
   check_status(dpvo_feature_pyramid_insert(src.data_ptr(), ptrs.data(), sc.data(),
-                                           (int)ptrs.size(), C, H, W, DPVO_F32, current_stream()),
+                                           (int)ptrs.size(), C, H, W, dtype_code(src),
+                                           current_stream()),
                "cuda_corr.feature_pyramid_insert");
 }
 

@@ -279,3 +279,67 @@ def test_ordered_corr_matches_unordered(gpu):
     b = altcorr.corr_levels(gmap, pyr, coords, kk1, jj1, 3, levels, order=order)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+# ---- fp16 features (MIXED_PRECISION): v_mfma_f32_16x16x16_f16 path ----
+# fp16 x fp16 products are exact in fp32 and the MFMA accumulates in fp32, so
+# against the fp64 oracle on the SAME fp16-rounded inputs only fp32 summation
+# noise remains: |gpu - ref| <= 2e-5 * max(1, |ref|_max).  (The reference's
+# fp16 path accumulates in fp16 -- an accuracy deviation in our favour.)
+@pytest.mark.parametrize("kw", [dict(), dict(spread=4.0), dict(far=0.3),
+                                dict(M=130, H2=12, W2=14)])
+@pytest.mark.parametrize("levels", [(1,), (1, 4), (1, 2, 4, 8)])
+def test_channels_last_fp16_matches_oracle(gpu, kw, levels):
+    from dpvo_amd import altcorr, synthetic
+
+    f1, f2, co, ii, jj, R = _case(13, **{**dict(M=67, C=128, H2=40, W2=48), **kw})
+    f1h = _t(f1, gpu, torch.float16)
+    lv1 = _t(f2, gpu, torch.float16)
+    pyr = [lv1 if s == 1 else
+           torch.nn.functional.avg_pool2d(lv1[0].float(), s, s).half().unsqueeze(0)
+           for s in levels]
+    out = altcorr.corr_levels(f1h, [synthetic.channels_last(p) for p in pyr], _t(co, gpu),
+                              _t(ii, gpu), _t(jj, gpu), R, scales=levels)
+    assert out.dtype == torch.float32
+    out = out.view(1, len(ii), 2 * R + 1, 2 * R + 1, 3, 3, len(levels)).cpu().numpy()
+    a = f1h.double().cpu().numpy()
+    for l, s in enumerate(levels):
+        ref = oracle.corr_fwd(a, pyr[l].double().cpu().numpy(), co / s, ii, jj, R)
+        _close(out[..., l], ref, 2e-5)
+
+
+def test_channels_last_fp16_equals_fp32_on_rounded_inputs(gpu):
+    """The fp16 and fp32 matrix-core kernels agree on fp16-representable
+    inputs at the full cfg2 edge count (only the K order differs)."""
+    from dpvo_amd import altcorr, fastba, synthetic
+
+    G = synthetic.make_config("cfg2", seed=6)
+    D = G.to(gpu)
+    mem, levels = 36, (1, 4)
+    coords, order = fastba.reproject(D.poses, D.patches, D.intrinsics, D.ii, D.jj, D.kk, mem=mem)
+    pyr = synthetic.make_features(mem=mem, C=128, levels=levels, seed=2, device=gpu)
+    pyr16 = [synthetic.channels_last(p.half()) for p in pyr]
+    pyr32 = [synthetic.channels_last(p.half().float()) for p in pyr]
+    gmap = (0.25 * torch.randn(1, mem * G.M, 128, 3, 3, device=gpu)).half()
+    kk1, jj1 = D.kk % (mem * G.M), D.jj % mem
+    a = altcorr.corr_levels(gmap, pyr16, coords, kk1, jj1, 3, levels, order=order)
+    b = altcorr.corr_levels(gmap.float(), pyr32, coords, kk1, jj1, 3, levels, order=order)
+    torch.cuda.synchronize()
+    err = (a - b).abs().max().item()
+    assert err <= 1e-5 * max(1.0, b.abs().max().item()), err
+
+
+@pytest.mark.parametrize("H,W,scales", [(120, 160, (1, 2, 4, 8)), (37, 45, (1, 2, 4, 8))])
+def test_insert_frame_fp16(gpu, H, W, scales):
+    """fp16 insertion: level 1 copied exactly, pooled levels = fp32 avg_pool2d
+    of the halves rounded once to fp16 (torch's half avg_pool2d semantics)."""
+    from dpvo_amd import altcorr, synthetic
+
+    fmap = torch.randn(128, H, W, device=gpu).half()
+    pyr = [synthetic.channels_last(torch.full((1, 3, 128, H // s, W // s), 7.0, device=gpu,
+                                              dtype=torch.float16)) for s in scales]
+    altcorr.insert_frame(fmap, pyr, 1, scales)
+    for p, s in zip(pyr, scales):
+        ref = fmap if s == 1 else torch.nn.functional.avg_pool2d(fmap[None].float(), s, s)[0].half()
+        assert torch.equal(p[0, 1], ref), s
+        assert bool((p[0, [0, 2]] == 7.0).all())
