@@ -73,6 +73,15 @@ struct CorrT<__half> {
   static constexpr int kLaneCh = 32;
 };
 
+// wave-uniform per-level parameter without a dynamic index into the kernel
+// argument struct (that would route every access through scratch / flat
+// loads, which count in vmcnt and force full drains in the tile loop)
+template <typename X>
+__device__ __forceinline__ X sel4(int l, X a, X b, X c, X d) {
+  return l == 0 ? a : l == 1 ? b : l == 2 ? c : d;
+}
+#define LV_SEL(field, l) sel4((l), lv.field[0], lv.field[1], lv.field[2], lv.field[3])
+
 __device__ __forceinline__ f16x4 h4_lo(const uint4& v) {
   f16x4 r;
   __builtin_memcpy(&r, &v.x, 8);
@@ -98,7 +107,9 @@ __device__ __forceinline__ f16x4 h4_hi(const uint4& v) {
 //  * a level's bilinear + permute runs as soon as its last tile is in LDS,
 //    from per-lane output codes computed once (no integer division per level).
 
-template <typename T>
+// RAW9: p = 3, R = 3 (DPVO): the bilinear runs on the raw (2R+2)^2 = 64 grid
+// with one lane per raw point (see below); otherwise one lane per output.
+template <typename T, bool RAW9>
 __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 waves) per CU: every edge resident at once
     corr_nhwc_kernel(const T* __restrict__ fmap1, NhwcLevels lv, int L,
                      const float* __restrict__ coords, const int64_t* __restrict__ ii,
@@ -184,7 +195,7 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     const int gl = lane >> 4, gk = lane & 15;
     const bool act = gl < L && gk < np;
     const float xr = __shfl(cv, min(gk, np - 1), kWave), yr = __shfl(cv, np + min(gk, np - 1), kWave);
-    const float sc = lv.scale[gl < L ? gl : 0];
+    const float sc = LV_SEL(scale, gl < L ? gl : 0);
     const bool pow2 = (__float_as_uint(sc) & 0x7fffffu) == 0u;  // x / 2^k == x * 2^-k
     const float rs = 1.0f / sc;
     const float x = pow2 ? xr * rs : xr / sc, y = pow2 ? yr * rs : yr / sc;
@@ -205,7 +216,7 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
       yhi = max(yhi, __shfl_xor(yhi, o, kWave));
     }
     if (gk == 0 && gl < L) {
-      const int H2 = lv.H2[gl], W2 = lv.W2[gl];
+      const int H2 = LV_SEL(H2, gl), W2 = LV_SEL(W2, gl);
       xlo = max(xlo - R, 0);
       ylo = max(ylo - R, 0);
       xhi = min(xhi + R + 1, W2 - 1);
@@ -235,32 +246,69 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   }
   CORR_STAMP(1);
 
-  // ---- per-lane output codes o = lane + 64u -> (k, yy, xx), once
-  int code[kOutPerLane];
+  // ---- outputs.  Generic: lane owns outputs o = lane + 64u, decoded once
+  // into (k, yy, xx).  RAW9: lane = (rx, ry) = (lane >> 3, lane & 7) owns the
+  // raw window point (rx, ry) of every patch pixel k and, for rx, ry < 7, the
+  // outputs (k, yy = ry, xx = rx) of every k: o = (rx * 7 + ry) * 9 + k, i.e.
+  // 9 x L contiguous floats per lane.
+  constexpr int kOuts = RAW9 ? 9 : kOutPerLane;
+  int code[RAW9 ? 1 : kOutPerLane];
+  if constexpr (!RAW9) {
 #pragma unroll
-  for (int u = 0; u < kOutPerLane; u++) {
-    const int o = lane + kWave * u;
-    const int k = o % np, t = o / np, yy = t % Dp, xx = t / Dp;
-    code[u] = (o < nout) ? (k | (yy << 8) | (xx << 16)) : -1;
+    for (int u = 0; u < kOutPerLane; u++) {
+      const int o = lane + kWave * u;
+      const int k = o % np, t = o / np, yy = t % Dp, xx = t / Dp;
+      code[u] = (o < nout) ? (k | (yy << 8) | (xx << 16)) : -1;
+    }
   }
-  float outv[kOutPerLane][kMaxL];
+  const int rx = lane >> 3, ry = lane & 7;
+  float outv[kOuts][kMaxL];
 #pragma unroll
-  for (int u = 0; u < kOutPerLane; u++)
+  for (int u = 0; u < kOuts; u++)
 #pragma unroll
     for (int ll = 0; ll < kMaxL; ll++) outv[u][ll] = 0.f;
 
   // bilinear + permute of level l from G (correlation_kernel.cu:260-271).
   // Branch-free: every tap is loaded from a clamped (valid) LDS address and
-  // zeroed by a select, so the 32 LDS reads of a level issue back to back
-  // instead of one branch (and one LDS round trip) per tap.
-  auto bilinear = [&](int l, bool fast) {
+  // zeroed by a select.  RAW9: each lane loads ONE raw value per k, the other
+  // three taps come from lanes +1 (y + 1), +8 (x + 1), +9 by cross-lane
+  // shuffles: 9 LDS reads per lane and level instead of 32.
+  auto bilinear_raw = [&](int l, bool fast) __attribute__((always_inline)) {
     const NhwcGeom* gg = geo + l;
     const int xlo = wave_uniform(gg->xlo), ylo = wave_uniform(gg->ylo);
     const int bw = wave_uniform(gg->bw), bh = wave_uniform(gg->bh);
     const int cap = max(bw * bh - 1, 0);
 #pragma unroll
-    for (int u = 0; u < kOutPerLane; u++) {
-      const int cd = max(code[u], 0);
+    for (int k = 0; k < 9; k++) {
+      float r;
+      if (fast) {
+        const int gy = gg->y0[k] + ry - R - ylo, gx = gg->x0[k] + rx - R - xlo;
+        const bool in = gy >= 0 && gy < bh && gx >= 0 && gx < bw;
+        const float a = G[k * kBoxStride + min(max(gy * bw + gx, 0), cap)];
+        r = in ? a : 0.f;
+      } else {
+        r = G[k * 64 + ry * 8 + rx];
+      }
+      const float r10 = __shfl_down(r, 1, kWave);   // (y + 1, x)
+      const float r01 = __shfl_down(r, 8, kWave);   // (y, x + 1)
+      const float r11 = __shfl_down(r, 9, kWave);   // (y + 1, x + 1)
+      const float dx = gg->dx[k], dy = gg->dy[k];
+      float v = ((1.f - dx) * (1.f - dy)) * r;
+      v = v + (dx * (1.f - dy)) * r01;
+      v = v + ((1.f - dx) * dy) * r10;
+      v = v + (dx * dy) * r11;
+#pragma unroll
+      for (int ll = 0; ll < kMaxL; ll++) outv[k][ll] = (ll == l) ? v : outv[k][ll];
+    }
+  };
+  auto bilinear_gen = [&](int l, bool fast) __attribute__((always_inline)) {
+    const NhwcGeom* gg = geo + l;
+    const int xlo = wave_uniform(gg->xlo), ylo = wave_uniform(gg->ylo);
+    const int bw = wave_uniform(gg->bw), bh = wave_uniform(gg->bh);
+    const int cap = max(bw * bh - 1, 0);
+#pragma unroll
+    for (int u = 0; u < kOuts; u++) {
+      const int cd = max(code[RAW9 ? 0 : u], 0);
       const int k = cd & 0xff, yy = (cd >> 8) & 0xff, xx = cd >> 16;
       float r00, r01, r10, r11;
       if (fast) {
@@ -289,18 +337,22 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
       v = v + (dx * (1.f - dy)) * r01;
       v = v + ((1.f - dx) * dy) * r10;
       v = v + (dx * dy) * r11;
-      v = (code[u] >= 0) ? v : 0.f;
+      v = (code[RAW9 ? 0 : u] >= 0) ? v : 0.f;
 #pragma unroll
       for (int ll = 0; ll < kMaxL; ll++) outv[u][ll] = (ll == l) ? v : outv[u][ll];
     }
+  };
+  auto bilinear = [&](int l, bool fast) __attribute__((always_inline)) {
+    if constexpr (RAW9) bilinear_raw(l, fast);
+    else bilinear_gen(l, fast);
   };
 
   // levels off the fast path (empty box, or windows too spread for it) first
   for (int l = 0; l < L; l++) {
     const int nt = wave_uniform(geo[l].ntile);
     if (nt > kMaxTiles) {  // raw[k][yy][xx] directly into G
-      const int H2 = lv.H2[l], W2 = lv.W2[l];
-      const T* f2 = static_cast<const T*>(lv.f2[l]) + ((size_t)b * N2 + jx) * H2 * W2 * C;
+      const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
+      const T* f2 = static_cast<const T*>(LV_SEL(f2, l)) + ((size_t)b * N2 + jx) * H2 * W2 * C;
       for (int e = lane; e < np * D * D; e += kWave) {
         const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
         const int i1 = geo[l].y0[k] + yy - R, j1 = geo[l].x0[k] + xx - R;
@@ -321,8 +373,8 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   }
 
   // ---- flattened fast-path tiles, kRing - 1 in flight
-  const int nT = cum[L];
-  auto tile_src = [&](int i) -> const T* {
+  const int nT = cum[kMaxL];  // == cum[L]: positions >= L add no tiles
+  auto tile_src = [&](int i) __attribute__((always_inline)) -> const T* {
     i = min(i, max(nT - 1, 0));  // past the end: re-read the last tile (never used)
     const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
     const int t = i - (j == 0 ? 0 : j == 1 ? cum[1] : j == 2 ? cum[2] : cum[3]);
@@ -332,8 +384,8 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     const float rbw = 1.0f / (float)max(bw0, 1);
     const int px = min(16 * t + ai, max(npx - 1, 0));  // pad columns read pixel npx-1
     const int r = (int)(((float)px + 0.5f) * rbw), cc = px - r * max(bw0, 1);
-    const int H2 = lv.H2[l], W2 = lv.W2[l];
-    const T* f2 = static_cast<const T*>(lv.f2[l]) + ((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 * C;
+    const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
+    const T* f2 = static_cast<const T*>(LV_SEL(f2, l)) + ((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 * C;
     return f2 + ((size_t)(wave_uniform(gg->ylo) + r) * W2 + wave_uniform(gg->xlo) + cc) * C +
            CorrT<T>::kLaneCh * aq;
   };
@@ -342,26 +394,34 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     return *reinterpret_cast<const uint4*>(s + (kHalf ? 8 * h : 16 * h));
   };
   if (nT > 0) {
-    // register ring: cur = tile i, n1 / n2 = tiles i + 1, i + 2 in flight;
-    // one loop body (rotation by register moves, which issue in the MFMA
-    // shadow) keeps the kernel small enough for the instruction cache
+    // register ring of three tiles, rotated by NAME (the loop is unrolled by
+    // three): while tile i multiplies, tiles i + 1 and i + 2 are in flight and
+    // the wait before tile i only drains tile i's own loads.  (A rotation by
+    // register moves forces a full vmcnt(0) drain every tile: moving the
+    // youngest tile's registers waits for its loads.)
     constexpr int V = CorrT<T>::kVecs;
-    uint4 cur[V], n1[V], n2[V];
+    uint4 ra[V], rb[V], rc[V];
     {
       const T* s0 = tile_src(0);
       const T* s1 = tile_src(1);
       const T* s2 = tile_src(2);
+      // issue order ra, rb, rc (sched barriers): the wait before the first
+      // tile then drains only ra's loads
 #pragma unroll
-      for (int h = 0; h < V; h++) cur[h] = tile_vec(s0, h);
+      for (int h = 0; h < V; h++) ra[h] = tile_vec(s0, h);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int h = 0; h < V; h++) n1[h] = tile_vec(s1, h);
+      for (int h = 0; h < V; h++) rb[h] = tile_vec(s1, h);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int h = 0; h < V; h++) n2[h] = tile_vec(s2, h);
+      for (int h = 0; h < V; h++) rc[h] = tile_vec(s2, h);
     }
-    for (int i = 0; i < nT; i++) {
+    auto step = [&](uint4 (&cur)[V], int i) __attribute__((always_inline)) {
       // two accumulators (even / odd channel groups): two independent MFMA
       // chains, summed once per tile in a fixed order
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      const bool live = i < nT;  // the last group may hold 1-2 slots past the end
+      if (live) {
       if constexpr (kHalf) {
         // 8 K steps of 16 channels: vector h holds steps 2h (lo) and 2h + 1 (hi)
 #pragma unroll
@@ -384,16 +444,15 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
           acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 7], c1.w, acc1, 0, 0, 0);
         }
       }
-#pragma unroll
-      for (int h = 0; h < V; h++) {
-        cur[h] = n1[h];
-        n1[h] = n2[h];
       }
-      {  // tile i + 3 (past the end: the last tile again, never used)
+      {  // refill this slot with tile i + 3 (past the end: the last tile again, never
+         // used); unconditional, so every path into the next group has the same
+         // load order and the wait before a tile drains only that tile's loads
         const T* src = tile_src(i + 3);
 #pragma unroll
-        for (int h = 0; h < V; h++) n2[h] = tile_vec(src, h);
+        for (int h = 0; h < V; h++) cur[h] = tile_vec(src, h);
       }
+      if (!live) return;
       const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
       const int lb = (j == 0 ? 0 : j == 1 ? cum[1] : j == 2 ? cum[2] : cum[3]);
       const int t = i - lb, l = level_at(j);
@@ -411,25 +470,51 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
         wave_lds_sync();
         CORR_STAMP(3 + 2 * l);
       }
+    };
+    // no early exit inside a group: a break path into the loop's flow block
+    // would make the compiler wait for every outstanding load at the top
+    for (int i = 0; i < nT; i += 3) {
+      step(ra, i);
+      step(rb, i + 1);
+      step(rc, i + 2);
     }
   }
 
   // ---- one contiguous [nout][L] row block per edge
   CORR_STAMP(10);
   float* dst = out + ((size_t)b * M + m) * nout * L;
+  if constexpr (RAW9) {
+    if (rx < 7 && ry < 7) {
+      float* d = dst + (size_t)(rx * 7 + ry) * 9 * L;
 #pragma unroll
-  for (int u = 0; u < kOutPerLane; u++) {
-    const int o = lane + kWave * u;
-    if (o >= nout) continue;
-    if (L == 4) {
-      *reinterpret_cast<float4*>(dst + (size_t)o * 4) =
-          make_float4(outv[u][0], outv[u][1], outv[u][2], outv[u][3]);
-    } else if (L == 2) {
-      *reinterpret_cast<float2*>(dst + (size_t)o * 2) = make_float2(outv[u][0], outv[u][1]);
-    } else {
+      for (int k = 0; k < 9; k++) {
+        if (L == 4) {
+          *reinterpret_cast<float4*>(d + 4 * k) =
+              make_float4(outv[k][0], outv[k][1], outv[k][2], outv[k][3]);
+        } else if (L == 2) {
+          *reinterpret_cast<float2*>(d + 2 * k) = make_float2(outv[k][0], outv[k][1]);
+        } else {
 #pragma unroll
-      for (int ll = 0; ll < kMaxL; ll++)
-        if (ll < L) dst[(size_t)o * L + ll] = outv[u][ll];
+          for (int ll = 0; ll < kMaxL; ll++)
+            if (ll < L) d[k * L + ll] = outv[k][ll];
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kOutPerLane; u++) {
+      const int o = lane + kWave * u;
+      if (o >= nout) continue;
+      if (L == 4) {
+        *reinterpret_cast<float4*>(dst + (size_t)o * 4) =
+            make_float4(outv[u][0], outv[u][1], outv[u][2], outv[u][3]);
+      } else if (L == 2) {
+        *reinterpret_cast<float2*>(dst + (size_t)o * 2) = make_float2(outv[u][0], outv[u][1]);
+      } else {
+#pragma unroll
+        for (int ll = 0; ll < kMaxL; ll++)
+          if (ll < L) dst[(size_t)o * L + ll] = outv[u][ll];
+      }
     }
   }
   CORR_STAMP(11);
@@ -637,14 +722,26 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   const bool ordered = order && B == 1;
   if (ordered) grid = 8u * (unsigned)((grid + 7) / 8);
   const int* ord = ordered ? (const int*)order : (const int*)nullptr;
-  if (dtype == DPVO_F16)
-    hipLaunchKernelGGL(corr_nhwc_kernel<__half>, dim3(grid), dim3(kNhwcWaves * kWave), smem,
-                       as_stream(stream), (const __half*)fmap1, lv, L, coords, ii, jj, B, M, np,
-                       N1, N2, radius, ord, out);
-  else
-    hipLaunchKernelGGL(corr_nhwc_kernel<float>, dim3(grid), dim3(kNhwcWaves * kWave), smem,
-                       as_stream(stream), (const float*)fmap1, lv, L, coords, ii, jj, B, M, np,
-                       N1, N2, radius, ord, out);
+  const bool raw9 = np == 9 && radius == 3;  // DPVO: p = 3, R = 3
+  const dim3 g(grid), blk(kNhwcWaves * kWave);
+  hipStream_t st = as_stream(stream);
+  if (dtype == DPVO_F16) {
+    const __half* f1 = (const __half*)fmap1;
+    if (raw9)
+      hipLaunchKernelGGL((corr_nhwc_kernel<__half, true>), g, blk, smem, st, f1, lv, L, coords, ii,
+                         jj, B, M, np, N1, N2, radius, ord, out);
+    else
+      hipLaunchKernelGGL((corr_nhwc_kernel<__half, false>), g, blk, smem, st, f1, lv, L, coords,
+                         ii, jj, B, M, np, N1, N2, radius, ord, out);
+  } else {
+    const float* f1 = (const float*)fmap1;
+    if (raw9)
+      hipLaunchKernelGGL((corr_nhwc_kernel<float, true>), g, blk, smem, st, f1, lv, L, coords, ii,
+                         jj, B, M, np, N1, N2, radius, ord, out);
+    else
+      hipLaunchKernelGGL((corr_nhwc_kernel<float, false>), g, blk, smem, st, f1, lv, L, coords,
+                         ii, jj, B, M, np, N1, N2, radius, ord, out);
+  }
   return launch_status();
 }
 

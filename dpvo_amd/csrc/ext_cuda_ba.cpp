@@ -368,38 +368,65 @@ std::vector<torch::Tensor> ba_solve_system(torch::Tensor J_Ginv_i, torch::Tensor
   TORCH_CHECK(J_Ginv_i.numel() == 49 * r && J_Ginv_j.numel() == 49 * r,
               "J_Ginv_i / J_Ginv_j must be [r, 7, 7]");
   TORCH_CHECK(ii.numel() == r && jj.numel() == r, "ii / jj must be [r]");
-  // the reference calls exit(1) on a self edge (ba.cpp:150-151); raise instead
-  // one device->host sync for all index checks (the reference syncs on ii.max())
-  const auto st = torch::stack({(ii == jj).any().to(torch::kInt64),
-                                torch::minimum(ii.min(), jj.min()),
-                                torch::maximum(ii.max(), jj.max())})
-                      .cpu();
-  const int64_t* sv = st.data_ptr<int64_t>();
-  TORCH_CHECK(sv[0] == 0, "cuda_ba.solve_system: edge with ii == jj");
-  TORCH_CHECK(sv[1] >= 0, "cuda_ba.solve_system: negative pose index");
-  const int64_t n = sv[2] + 1;
-  const auto opt64 = res.options().dtype(torch::kFloat64);
-  auto A = torch::empty({7 * n, 7 * n}, opt64);
-  auto b = torch::empty({7 * n}, opt64);
-  check_status(dpvo_pgo_assemble(J_Ginv_i.data_ptr<float>(), J_Ginv_j.data_ptr<float>(),
-                                 ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(),
-                                 res.data_ptr<float>(), (int)r, (int)n, (float)ep, (float)lm,
-                                 A.data_ptr<double>(), b.data_ptr<double>(), current_stream()),
-               "cuda_ba.solve_system");
-  int64_t f = (int64_t)freen * 7;  // solve(A, b, freen*7): < 0 -> whole system
-  if (f < 0 || f > 7 * n) f = 7 * n;
-  auto delta = torch::zeros({7 * n}, opt64);
-  if (f > 0) {
-    auto As = A.narrow(0, 0, f).narrow(1, 0, f);
-    auto chol = at::linalg_cholesky_ex(As);
-    const int64_t info = std::get<1>(chol).item<int64_t>();
-    TORCH_CHECK(info == 0, "cuda_ba.solve_system: the damped pose-graph system is not positive "
-                "definite (Cholesky info ", info, "); check for NaN residuals/Jacobians or "
-                "unconstrained poses with ep = 0");
-    delta.narrow(0, 0, f).copy_(
-        at::cholesky_solve(b.narrow(0, 0, f).unsqueeze(1), std::get<0>(chol)).squeeze(1));
+  // The structure (which poses a long edge touches) is host logic, as in the
+  // reference (ba.cpp:141-158 builds the triplets on the host): one copy of
+  // the indices to the host, which also does the reference's checks.
+  const auto iih = ii.cpu(), jjh = jj.cpu();
+  const int64_t* ip = iih.data_ptr<int64_t>();
+  const int64_t* jp = jjh.data_ptr<int64_t>();
+  int64_t n = 0;
+  for (int64_t x = 0; x < r; x++) {
+    // the reference calls exit(1) on a self edge (ba.cpp:150-151); raise instead
+    TORCH_CHECK(ip[x] != jp[x], "cuda_ba.solve_system: edge with ii == jj");
+    TORCH_CHECK(ip[x] >= 0 && jp[x] >= 0, "cuda_ba.solve_system: negative pose index");
+    n = std::max(n, std::max(ip[x], jp[x]) + 1);
   }
-  return {delta.to(torch::kFloat32).view({n, 7}).to(out_dev)};
+  int64_t nf = freen;  // solve(A, b, freen*7): < 0 (or past the end) -> whole system
+  if (nf < 0 || nf > n) nf = n;
+  auto delta = torch::zeros({n, 7}, res.options().dtype(torch::kFloat64));
+  if (nf > 0) {
+    TORCH_CHECK(nf < (1LL << 30), "cuda_ba.solve_system: too many poses");
+    int64_t len = 0;
+    check_status(dpvo_pgo_plan(ip, jp, (int)r, (int)nf, nullptr, 0, &len), "cuda_ba.solve_system");
+    auto planh = torch::empty({len}, torch::kInt64);
+    check_status(dpvo_pgo_plan(ip, jp, (int)r, (int)nf, planh.data_ptr<int64_t>(), len, &len),
+                 "cuda_ba.solve_system");
+    const int64_t* hdr = planh.data_ptr<int64_t>();
+    const int64_t m = hdr[3], ws_n = hdr[25], hS = hdr[22], hBB = hdr[23], hDelta = hdr[24];
+    auto plan = planh.to(dev, /*non_blocking=*/false);
+    auto ws = torch::empty({ws_n}, res.options().dtype(torch::kFloat64));
+    auto fail = torch::zeros({1}, res.options().dtype(torch::kInt32));
+    check_status(dpvo_pgo_factor(J_Ginv_i.data_ptr<float>(), J_Ginv_j.data_ptr<float>(),
+                                 ii.data_ptr<int64_t>(), res.data_ptr<float>(),
+                                 plan.data_ptr<int64_t>(), hdr, (float)ep, (float)lm,
+                                 ws.data_ptr<double>(), fail.data_ptr<int>(), current_stream()),
+                 "cuda_ba.solve_system");
+    torch::Tensor xB, info = torch::zeros({1}, res.options().dtype(torch::kInt32));
+    if (m > 0) {  // dense SPD solve of the border system (7 m unknowns)
+      auto S = ws.narrow(0, hS, 49 * m * m).view({7 * m, 7 * m});
+      auto bB = ws.narrow(0, hBB, 7 * m);
+      auto chol = at::linalg_cholesky_ex(S);
+      info = std::get<1>(chol).to(torch::kInt32).view({1});
+      xB = at::cholesky_solve(bB.unsqueeze(1), std::get<0>(chol)).squeeze(1).contiguous();
+    }
+    check_status(dpvo_pgo_back(plan.data_ptr<int64_t>(), hdr,
+                               m > 0 ? xB.data_ptr<double>() : nullptr, ws.data_ptr<double>(),
+                               current_stream()),
+                 "cuda_ba.solve_system");
+    delta.narrow(0, 0, nf).copy_(ws.narrow(0, hDelta, 7 * nf).view({nf, 7}));
+    if (m > 0) {
+      auto bidx = planh.narrow(0, hdr[7], 3 * m).view({m, 3}).select(1, 0).contiguous().to(dev);
+      delta.index_copy_(0, bidx, xB.view({m, 7}));
+    }
+    // one device->host sync for both failure reports
+    const auto st = torch::cat({fail, info}).cpu();
+    const int* sv = st.data_ptr<int>();
+    TORCH_CHECK(sv[0] == 0 && sv[1] == 0,
+                "cuda_ba.solve_system: the damped pose-graph system is not positive definite "
+                "(segment pivot failure ", sv[0], ", border Cholesky info ", sv[1],
+                "); check for NaN residuals/Jacobians or unconstrained poses with ep = 0");
+  }
+  return {delta.to(torch::kFloat32).to(out_dev)};
 }
 
 // Split F-BA for the edge-sharded multi-GPU path.

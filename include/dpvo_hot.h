@@ -159,6 +159,31 @@ int dpvo_pgo_assemble(const float* J_Ginv_i, const float* J_Ginv_j, const int64_
                       const int64_t* jj, const float* res, int r, int n, float ep, float lm,
                       double* A, double* b, void* stream);
 
+/* Structured sparse solve of the same system (the default path of
+   cuda_ba.solve_system, replacing Eigen SimplicialCholesky, ba.cpp:99-180).
+   Poses touched by a long edge (|i - j| > 1) form a dense "border"; the other
+   free poses form chain segments that are block-tridiagonal.
+   dpvo_pgo_plan (HOST arrays ii / jj [r]; nf = number of free poses, i.e.
+   the reference's freen, or n): call with plan == NULL to get the length in
+   int64 words, then again to fill it.  The plan's first 32 words are its
+   header (counts, table offsets, workspace offsets in doubles; word 25 = the
+   workspace length, 3 = m border poses, 22 / 23 = offsets of the dense border
+   matrix [7m, 7m] and its right-hand side, 24 = the [nf, 7] step; the border
+   table at word 7 holds (pose, left segment, right segment) triples).
+   dpvo_pgo_factor (device plan, host copy of the header `hdr`): zeroes the
+   workspace, assembles every 7x7 block (edges summed in ascending order:
+   deterministic), factors the segments and folds their Schur terms into the
+   border system; *fail (device int) = 1 if a segment pivot is not positive.
+   The caller solves the border system (dense SPD) into xB [m, 7];
+   dpvo_pgo_back back-substitutes the segments. */
+int dpvo_pgo_plan(const int64_t* ii, const int64_t* jj, int r, int nf, int64_t* plan,
+                  int64_t plan_cap, int64_t* plan_len);
+int dpvo_pgo_factor(const float* J_Ginv_i, const float* J_Ginv_j, const int64_t* ii,
+                    const float* res, const int64_t* plan, const int64_t* hdr, float ep, float lm,
+                    double* ws, int* fail, void* stream);
+int dpvo_pgo_back(const int64_t* plan, const int64_t* hdr, const double* xB, double* ws,
+                  void* stream);
+
 /* Largest number of free poses (t1 - t0) dpvo_ba_forward handles. */
 int dpvo_ba_max_free_poses(void);
 

@@ -103,7 +103,16 @@ int main(int argc, char** argv) {
   hipMalloc(&dout, (size_t)E * 49 * 9 * L * 4);
   hipMalloc(&dst, (size_t)E * 16 * 8);
   hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dst, sizeof(dst));
-  const void* f2[4] = {lvl[0], lvl[1], lvl[2], lvl[3]};
+  // optional level subset: corr_bench <ordered> <first level> <count>
+  const int l0 = argc > 2 ? atoi(argv[2]) : 0, Lr = argc > 3 ? atoi(argv[3]) : L;
+  const void* f2[4] = {lvl[l0 % 4], lvl[(l0 + 1) % 4], lvl[(l0 + 2) % 4], lvl[(l0 + 3) % 4]};
+  int H2r[4], W2r[4];
+  float scr[4];
+  for (int l = 0; l < 4; l++) {
+    H2r[l] = H2[(l0 + l) % 4];
+    W2r[l] = W2[(l0 + l) % 4];
+    scr[l] = sc[(l0 + l) % 4];
+  }
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
@@ -111,7 +120,7 @@ int main(int argc, char** argv) {
   for (int r = 0; r < 60; r++) {
     hipMemset(dst, 0, (size_t)E * 16 * 8);
     hipEventRecord(a, 0);
-    int st = dpvo_corr_forward_levels_nhwc_ordered(gmap, f2, H2, W2, sc, L, dco, dii, djj,
+    int st = dpvo_corr_forward_levels_nhwc_ordered(gmap, f2, H2r, W2r, scr, Lr, dco, dii, djj,
                                                    ordered ? dord : nullptr, 1, E, C, P, P,
                                                    mem * Mp, mem, R, DPVO_F32, dout, 0);
     hipEventRecord(b, 0);
