@@ -30,7 +30,7 @@ INCLUDE = os.path.join(REPO, "include")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("DPVO_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["corr.hip", "corr_nhwc.hip", "ba.hip", "ba_fused.hip", "ba_blocks.hip", "ba_window.hip", "ba_large.hip", "lie.hip", "pgo.hip", "pg.hip"]
+HIP_SOURCES = ["corr.hip", "corr_nhwc.hip", "ba.hip", "ba_window.hip", "ba_large.hip", "lie.hip", "pgo.hip", "pg.hip"]
 EXTENSIONS = {
     "cuda_corr": "ext_cuda_corr.cpp",
     "cuda_ba": "ext_cuda_ba.cpp",
@@ -41,7 +41,7 @@ HEADERS = ["common.hpp", "ext_common.hpp", "ba_device.hpp", "ba_solve.hpp"]
 # steps run by few waves: clang's SLP vectoriser packs its scalar fp32 math into
 # v_pk_fma_f32 and pays for it with register-pair v_mov shuffles (3x the
 # instructions of the 6x6 pivot factorisation), so it is off there.
-SOURCE_FLAGS = {"ba_blocks.hip": ["-fno-slp-vectorize"], "ba_window.hip": ["-fno-slp-vectorize"]}
+SOURCE_FLAGS = {"ba_window.hip": ["-fno-slp-vectorize"]}
 
 
 def _git_rev():

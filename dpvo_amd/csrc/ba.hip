@@ -1062,20 +1062,7 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// ba_fused.hip: the single-workgroup whole-call kernel for DPVO-sized windows
-size_t ba_fused_scratch_bytes(int E, int N);
-bool ba_fused_supported(int E, int N, int P);
-int ba_fused_launch(float* poses, float* patches, const float* intrinsics, const float* target,
-                    const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
-                    const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
-                    int iterations, char* scratch, int* meta, int64_t* marks, void* stream);
-// ba_blocks.hip: one persistent workgroup per lower 6x6 block of S
-size_t ba_blocks_scratch_bytes(int E, int N);
-bool ba_blocks_supported(int E, int N, int P);
-int ba_blocks_launch(float* poses, float* patches, const float* intrinsics, const float* target,
-                     const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
-                     const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
-                     int iterations, char* scratch, int* meta, int64_t* marks, void* stream);
+
 // ba_window.hip: plan kernel + persistent per-block workgroups, solve in every workgroup
 size_t ba_window_scratch_bytes(int E, int N);
 bool ba_window_supported(int E, int N, int P);
@@ -1099,8 +1086,7 @@ int gba_forward(float* poses, float* patches, const float* intrinsics, const flo
 }  // namespace dpvo
 
 namespace {
-// 0 auto (window), 1 fused single workgroup, 2 multi-kernel, 3 blocks, 4 large-graph path,
-// 5 window
+// 0 auto (window), 2 multi-kernel, 4 large-graph path, 5 window (1 / 3 removed)
 int g_ba_path = 0;
 }
 
@@ -1161,8 +1147,7 @@ DPVO_EXPORT size_t dpvo_ba_workspace_bytes(int E, int t0, int t1) {
   const int Ep = E > 0 ? E : 1;
   size_t bytes = 0;
   if (window_path_ok(Ep, N)) {
-    size_t a = ba_fused_scratch_bytes(Ep, N), b = ba_blocks_scratch_bytes(Ep, N);
-    a = a > b ? a : b;
+    size_t a = 0;
     if (ba_window_supported(Ep, N, 3)) {
       const size_t c = ba_window_scratch_bytes(Ep, N);
       a = a > c ? a : c;
@@ -1177,19 +1162,11 @@ DPVO_EXPORT size_t dpvo_ba_workspace_bytes(int E, int t0, int t1) {
 }
 
 DPVO_EXPORT int dpvo_ba_select_path(int mode) {
-  if (mode < 0 || mode > 5) return DPVO_ERR_INVALID;
+  if (mode < 0 || mode > 5 || mode == 1 || mode == 3) return DPVO_ERR_INVALID;
   g_ba_path = mode;
   return DPVO_OK;
 }
 
-namespace dpvo {
-void ba_blocks_set_refine(int on);
-}
-DPVO_EXPORT int dpvo_ba_set_refine(int on) {
-  if (on < 0 || on > 2) return DPVO_ERR_INVALID;
-  dpvo::ba_blocks_set_refine(on);
-  return DPVO_OK;
-}
 
 DPVO_EXPORT int dpvo_ba_max_free_poses(void) { return dpvo_gba_max_free_poses(); }
 
@@ -1348,14 +1325,6 @@ DPVO_EXPORT int dpvo_ba_forward(float* poses, float* patches, const float* intri
     return ba_window_launch(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
                             num_poses, num_patches, t0, t1, iterations,
                             (char*)workspace + base_bytes, w.meta + 1, w.tmark, stream);
-  if (g_ba_path == 3 && ba_blocks_supported(E, N, P))
-    return ba_blocks_launch(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
-                            num_poses, num_patches, t0, t1, iterations,
-                            (char*)workspace + base_bytes, w.meta, w.tmark, stream);
-  if (g_ba_path == 1 && ba_fused_supported(E, N, P))
-    return ba_fused_launch(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
-                           num_poses, num_patches, t0, t1, iterations,
-                           (char*)workspace + base_bytes, w.meta, w.tmark, stream);
   ensure_lds_limits();
   hipStream_t s = as_stream(stream);
   BaArgs a = make_args(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,

@@ -1,5 +1,5 @@
-// ba_device.hpp -- device code shared by the F-BA kernels (ba_fused.hip,
-// ba_blocks.hip): the reference's fp32 edge linearisation, block scan, the
+// ba_device.hpp -- device code shared by the F-BA window kernel (ba_window.hip,
+// via ba_solve.hpp): the reference's fp32 edge linearisation, block scan, the
 // 6x6 LDL^T pivot factorisation and small index helpers.
 #pragma once
 

@@ -739,7 +739,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     double* pc = yd + 6 * N;  // [G][kPart] copy of the partials
     {
       const int tot_p = kPart * A.G;
-      constexpr int kIn = 8;  // loads in flight per thread
+      constexpr int kIn = 24;  // loads in flight per thread: one round for G <= 146 (cfg2: 99)
       for (int t0_ = tid; t0_ < tot_p; t0_ += kIn * kWT) {
         double v[kIn];
 #pragma unroll

@@ -647,8 +647,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("reproject_ordered", &ba_reproject_ordered,
         "reproject + edge order by target frame (for cuda_corr.forward_levels(order=))");
   m.def("select_path", [](int mode) { check_status(dpvo_ba_select_path(mode), "select_path"); },
-        "F-BA implementation: 0 auto, 1 fused single workgroup, 2 multi-kernel, 3 blocks, 4 large-graph, 5 window");
-  m.def("set_refine", [](int on) { check_status(dpvo_ba_set_refine(on), "set_refine"); },
-        "dense pose solve: 2 = fp64 block LDL^T (default), 0 = fp32 Cholesky (reference precision), 1 = fp32 + one fp64 refinement step");
+        "F-BA implementation: 0 auto, 2 multi-kernel, 4 large-graph, 5 window");
   m.attr("native_library") = dpvo_version();
 }

@@ -134,20 +134,15 @@ int dpvo_patchify_backward(const void* grad, const float* coords, int B, int C, 
 size_t dpvo_ba_workspace_bytes(int E, int t0, int t1);
 
 /* Instrumentation / testing: which F-BA implementation dpvo_ba_forward uses.
-   0 = auto: one persistent workgroup per lower 6x6 block of S (ba_blocks.hip)
-   for E <= 2048 edges and N <= 16 free poses, the multi-kernel path (ba.hip)
-   for E <= 16384 and N <= 20, the large-graph path (ba_large.hip) beyond;
-   1 = the single-workgroup kernel (ba_fused.hip, E <= 2048, N <= 12);
-   2 = the multi-kernel path; 3 = same as 0; 4 = always the large-graph path.
-   Process-wide; call before sizing the workspace. */
+   0 = auto: the window kernel (ba_window.hip: plan kernel + one persistent
+   workgroup per share of a lower 6x6 block of S, dense solve in every
+   workgroup) for E <= 4096 edges and N <= 16 free poses, the multi-kernel
+   path (ba.hip) for E <= 16384 and N <= 20, the large-graph path
+   (ba_large.hip) beyond; 2 = the multi-kernel path; 4 = always the
+   large-graph path; 5 = same as 0.  1 and 3 (the round-1 single-workgroup
+   and per-block kernels) were removed: DPVO_ERR_INVALID.  Process-wide; call
+   before sizing the workspace. */
 int dpvo_ba_select_path(int mode);
-
-/* Dense pose solve of the default (blocks) path.  mode 2 (default): fp64
-   block LDL^T with a look-ahead pivot factorisation; 0: fp32 blocked Cholesky
-   (the reference's own precision, ba_cuda.cu:547-548); 1: fp32 Cholesky plus
-   one fp64 iterative-refinement step.  Measured on cfg2 (N = 11): 21 / 24 /
-   37 us per iteration for modes 2 / 0 / 1.  Process-wide. */
-int dpvo_ba_set_refine(int on);
 
 /* Sim3 pose-graph normal equations.  Replaces the host assembly of
    cuda_ba.solve_system (dpvo/fastba/ba.cpp:120-165): J_Ginv_i / J_Ginv_j

@@ -23,12 +23,12 @@ def cb(gpu):
     return dpvo_amd.load_extension("cuda_ba")
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["window", "fused", "multikernel", "blocks"])
+@pytest.fixture(params=[0, 2], ids=["window", "multikernel"])
 def path(request, cb):
     """F-BA implementation under test: 0 = auto (ba_window.hip: plan kernel +
     one persistent workgroup per share of a block of S, solve in every
-    workgroup), 1 = the single-workgroup kernel, 2 = the multi-kernel path,
-    3 = the round-1 per-block kernel (ba_blocks.hip)."""
+    workgroup), 2 = the multi-kernel path (ba.hip, DPVO windows above 4096
+    edges)."""
     cb.select_path(request.param)
     yield request.param
     cb.select_path(0)
@@ -118,16 +118,11 @@ def test_window_path_is_deterministic(cb, gpu):
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
-def test_fused_reruns_agree(cb, gpu):
-    # the single-workgroup kernel sums in fp64 with LDS atomics (order varies
-    # run to run, like the reference's fp32 atomics): reruns agree to fp32 rounding
-    cb.select_path(1)
-    G = synthetic.make_config("cfg2", seed=3)
-    a = _run_gpu(cb, G, gpu, 1, G.F, 2)
-    for _ in range(3):
-        b = _run_gpu(cb, G, gpu, 1, G.F, 2)
-        np.testing.assert_allclose(a[0], b[0], rtol=0, atol=1e-6)
-        np.testing.assert_allclose(a[1], b[1], rtol=1e-6, atol=1e-7)
+def test_removed_paths_rejected(cb, gpu):
+    # the round-1 single-workgroup (1) and per-block (3) kernels were removed
+    for mode in (1, 3):
+        with pytest.raises(RuntimeError):
+            cb.select_path(mode)
     cb.select_path(0)
 
 
@@ -260,20 +255,13 @@ def test_fused_general_graph_structure(cb, gpu, path, seed):
     _check(P, K, Pr, Kr)
 
 
-@pytest.mark.parametrize("refine", [0, 1, 2], ids=["fp32-solve", "fp32+fp64-refine", "fp64-ldl"])
-def test_blocks_solve_precision(cb, gpu, refine):
-    """The blocks path's dense solve modes -- fp32 Cholesky (the reference's
-    precision), fp32 + one fp64 refinement step, fp64 block LDL^T (the
-    default) -- all stay within the north_star tolerances of the fp64 oracle
-    on cfg2 (condition numbers ~2e5)."""
-    cb.set_refine(refine)
-    try:
-        for seed in (0, 4):
-            G = synthetic.make_config("cfg2", seed=seed)
-            P, K = _run_gpu(cb, G, gpu, 1, G.F, 2)
-            Pr, Kr = _run_oracle(G, 1, G.F, 2)
-            _check(P, K, Pr, Kr)
-            if refine:  # fp64-level solves: the oracle's up to the fp32 edge math
-                np.testing.assert_allclose(P, Pr, rtol=0, atol=2e-6)
-    finally:
-        cb.set_refine(2)
+def test_window_solve_precision(cb, gpu):
+    """The window kernel's dense solve (fp32 blocked Cholesky + one fp64
+    refinement step, ba_solve.hpp) stays at fp64-solve accuracy against the
+    fp64 oracle on cfg2 (condition numbers ~2e5)."""
+    for seed in (0, 4):
+        G = synthetic.make_config("cfg2", seed=seed)
+        P, K = _run_gpu(cb, G, gpu, 1, G.F, 2)
+        Pr, Kr = _run_oracle(G, 1, G.F, 2)
+        _check(P, K, Pr, Kr)
+        np.testing.assert_allclose(P, Pr, rtol=0, atol=2e-6)
