@@ -51,9 +51,13 @@ __device__ __forceinline__ int ifloor_safe(float v) {
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Order LDS traffic between lanes of ONE wave (a wave's DS ops execute in
-// order; this stops the compiler from moving them across the point).
+// order; this stops the compiler from moving them across the point).  The
+// fence is restricted to the LDS address space ("local"): a plain fence also
+// orders global memory and makes the compiler wait for every outstanding
+// global load (vmcnt(0)) at the point, which drains the load rings of the
+// streaming kernels (A-CORR's tile ring) at every use.
 __device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
 }
 

@@ -38,12 +38,22 @@ constexpr int kBoxStride = 16 * kMaxTiles + 4;  // +4: the 4 row groups of a G t
 constexpr int kMaxL = 4;        // levels per launch
 constexpr int kOutPerLane = 8;  // (2R+1)^2 * p*p <= 512 outputs per level
 constexpr int kNpMax = 16;      // p*p <= 16 (one MFMA row tile)
+// Box tiles per wave in the register ring (kRing - 1 in flight).  Measured
+// (scripts/micro/corr_bench, cfg2 shape): 3, 4 and 5 run within 3 % of each
+// other -- past the first level the loop is bound by the f32 MFMA issue rate,
+// not by load latency -- so the shallowest ring (fewest VGPRs) is kept.
+constexpr int kRing = 3;
 
 struct NhwcLevels {
   const void* f2[kMaxL];  // float or __half, [B, N2, H, W, C]
   int H2[kMaxL], W2[kMaxL];
   float scale[kMaxL];
 };
+
+// floats of a wave's output block: nout * L, rounded to whole float4s
+__host__ __device__ inline int corr_obuf_floats(int np, int R, int L) {
+  return ((2 * R + 1) * (2 * R + 1) * np * L + 3) & ~3;
+}
 
 struct NhwcGeom {
   int x0[kNpMax], y0[kNpMax];
@@ -53,6 +63,9 @@ struct NhwcGeom {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // 16-B tile vector (a native
+                                                                  // vector: a uint4 struct copy is a
+                                                                  // memcpy that keeps the ring in scratch)
 
 // fp16 features (DPVO's MIXED_PRECISION runtime, correlation_kernel.py:552-654):
 // v_mfma_f32_16x16x16_f16, fp32 accumulation (documented deviation: the
@@ -82,15 +95,13 @@ __device__ __forceinline__ X sel4(int l, X a, X b, X c, X d) {
 }
 #define LV_SEL(field, l) sel4((l), lv.field[0], lv.field[1], lv.field[2], lv.field[3])
 
-__device__ __forceinline__ f16x4 h4_lo(const uint4& v) {
-  f16x4 r;
-  __builtin_memcpy(&r, &v.x, 8);
-  return r;
+__device__ __forceinline__ f16x4 h4_lo(u32x4 v) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(f16x4, (u32x2){v.x, v.y});
 }
-__device__ __forceinline__ f16x4 h4_hi(const uint4& v) {
-  f16x4 r;
-  __builtin_memcpy(&r, &v.z, 8);
-  return r;
+__device__ __forceinline__ f16x4 h4_hi(u32x4 v) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(f16x4, (u32x2){v.z, v.w});
 }
 
 // One wave per edge, every level (the gmap patch and the coordinates are
@@ -119,6 +130,12 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   const int wid = wave_uniform(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
   float* G = smem + wid * (np * kBoxStride);
   NhwcGeom* geo = reinterpret_cast<NhwcGeom*>(smem + kNhwcWaves * np * kBoxStride) + wid * kMaxL;
+  // the edge's [nout][L] output block, assembled level by level (stored once,
+  // coalesced, at the end: no output registers held across the tile loop)
+  const int ostride = corr_obuf_floats(np, R, L);
+  float* obuf = reinterpret_cast<float*>(reinterpret_cast<NhwcGeom*>(smem + kNhwcWaves * np * kBoxStride) +
+                                         kNhwcWaves * kMaxL);
+  obuf += wid * ostride;
   int edge;
   if (order) {
     // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so
@@ -174,9 +191,10 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
 #pragma unroll
       for (int h = 0; h < kNhwcC / 16; h++)
 #pragma unroll
-        for (int s = 0; s < 4; s++)
+        for (int s = 0; s < 4; s++) {
           Afh[h][s] = arow ? (_Float16)__half2float(Gh[(32 * aq + 4 * h + s) * np + ai])
                            : (_Float16)0.0f;
+        }
     } else {
 #pragma unroll
       for (int h = 0; h < kNhwcC / 16; h++)
@@ -262,11 +280,6 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     }
   }
   const int rx = lane >> 3, ry = lane & 7;
-  float outv[kOuts][kMaxL];
-#pragma unroll
-  for (int u = 0; u < kOuts; u++)
-#pragma unroll
-    for (int ll = 0; ll < kMaxL; ll++) outv[u][ll] = 0.f;
 
   // bilinear + permute of level l from G (correlation_kernel.cu:260-271).
   // Branch-free: every tap is loaded from a clamped (valid) LDS address and
@@ -297,8 +310,7 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
       v = v + (dx * (1.f - dy)) * r01;
       v = v + ((1.f - dx) * dy) * r10;
       v = v + (dx * dy) * r11;
-#pragma unroll
-      for (int ll = 0; ll < kMaxL; ll++) outv[k][ll] = (ll == l) ? v : outv[k][ll];
+      if (rx < 7 && ry < 7) obuf[((rx * 7 + ry) * 9 + k) * L + l] = v;
     }
   };
   auto bilinear_gen = [&](int l, bool fast) __attribute__((always_inline)) {
@@ -337,9 +349,7 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
       v = v + (dx * (1.f - dy)) * r01;
       v = v + ((1.f - dx) * dy) * r10;
       v = v + (dx * dy) * r11;
-      v = (code[RAW9 ? 0 : u] >= 0) ? v : 0.f;
-#pragma unroll
-      for (int ll = 0; ll < kMaxL; ll++) outv[u][ll] = (ll == l) ? v : outv[u][ll];
+      if (code[RAW9 ? 0 : u] >= 0) obuf[(lane + kWave * u) * L + l] = v;
     }
   };
   auto bilinear = [&](int l, bool fast) __attribute__((always_inline)) {
@@ -374,95 +384,117 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
 
   // ---- flattened fast-path tiles, kRing - 1 in flight
   const int nT = cum[kMaxL];  // == cum[L]: positions >= L add no tiles
-  auto tile_src = [&](int i) __attribute__((always_inline)) -> const T* {
+  constexpr int V = CorrT<T>::kVecs;  // 16-B loads per lane per tile
+  // Per flattened position j (level level_at(j)): the box origin pointer, the
+  // box row stride, width, pixel count and 1 / width, materialised once in
+  // registers so the per-tile address math is a few selects on registers (no
+  // branches, no kernel-argument or LDS reads, no division per tile).
+  const T* pbase[kMaxL];
+  int prow[kMaxL], pbw[kMaxL], pnpx[kMaxL];
+  float prbw[kMaxL];
+#pragma unroll
+  for (int j = 0; j < kMaxL; j++) {
+    const int l = (j < L) ? level_at(j) : 0;
+    const NhwcGeom* gg = geo + l;
+    const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
+    const int bw0 = max(wave_uniform(gg->bw), 1);
+    pbw[j] = bw0;
+    pnpx[j] = bw0 * wave_uniform(gg->bh);
+    prbw[j] = 1.0f / (float)bw0;
+    prow[j] = W2 * C;
+    pbase[j] = static_cast<const T*>(LV_SEL(f2, l)) +
+               (((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 +
+                (size_t)wave_uniform(gg->ylo) * W2 + wave_uniform(gg->xlo)) * C;
+  }
+  auto pick = [](int j, auto a0, auto a1, auto a2, auto a3) __attribute__((always_inline)) {
+    return j == 0 ? a0 : j == 1 ? a1 : j == 2 ? a2 : a3;
+  };
+  // Tile i's loads: lane (i, q) reads 16 B of box pixel i directly in the MFMA
+  // B layout (16 pixels x 64 B per instruction).  (Whole-line loads staged
+  // through an LDS image and read back as B fragments measured 5-8 % slower.)
+  auto load_tile = [&](u32x4 (&dst)[V], int i) __attribute__((always_inline)) {
     i = min(i, max(nT - 1, 0));  // past the end: re-read the last tile (never used)
     const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
-    const int t = i - (j == 0 ? 0 : j == 1 ? cum[1] : j == 2 ? cum[2] : cum[3]);
-    const int l = level_at(j);
-    const NhwcGeom* gg = geo + l;
-    const int bw0 = wave_uniform(gg->bw), npx = bw0 * wave_uniform(gg->bh);
-    const float rbw = 1.0f / (float)max(bw0, 1);
-    const int px = min(16 * t + ai, max(npx - 1, 0));  // pad columns read pixel npx-1
-    const int r = (int)(((float)px + 0.5f) * rbw), cc = px - r * max(bw0, 1);
-    const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
-    const T* f2 = static_cast<const T*>(LV_SEL(f2, l)) + ((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 * C;
-    return f2 + ((size_t)(wave_uniform(gg->ylo) + r) * W2 + wave_uniform(gg->xlo) + cc) * C +
-           CorrT<T>::kLaneCh * aq;
-  };
-  // 16-B vector v of a lane's tile data: fp32 +16 h floats apart, fp16 contiguous
-  auto tile_vec = [&](const T* s, int h) -> uint4 {
-    return *reinterpret_cast<const uint4*>(s + (kHalf ? 8 * h : 16 * h));
+    const int t = i - pick(j, 0, cum[1], cum[2], cum[3]);
+    const T* base = pick(j, pbase[0], pbase[1], pbase[2], pbase[3]);
+    const int row = pick(j, prow[0], prow[1], prow[2], prow[3]);
+    const int bw0 = pick(j, pbw[0], pbw[1], pbw[2], pbw[3]);
+    const int npx = pick(j, pnpx[0], pnpx[1], pnpx[2], pnpx[3]);
+    const float rbw = pick(j, prbw[0], prbw[1], prbw[2], prbw[3]);
+    auto pix = [&](int q) __attribute__((always_inline)) -> int {  // element offset of box pixel 16t + q
+      const int px = min(16 * t + q, max(npx - 1, 0));  // pad columns read pixel npx-1
+      const int r = (int)(((float)px + 0.5f) * rbw), cc = px - r * bw0;
+      return r * row + cc * C;
+    };
+    {
+      const T* s = base + pix(ai) + CorrT<T>::kLaneCh * aq;
+#pragma unroll
+      for (int h = 0; h < V; h++)
+        dst[h] = *reinterpret_cast<const u32x4*>(s + (kHalf ? 8 * h : 16 * h));
+    }
   };
   if (nT > 0) {
-    // register ring of three tiles, rotated by NAME (the loop is unrolled by
-    // three): while tile i multiplies, tiles i + 1 and i + 2 are in flight and
-    // the wait before tile i only drains tile i's own loads.  (A rotation by
-    // register moves forces a full vmcnt(0) drain every tile: moving the
-    // youngest tile's registers waits for its loads.)
-    constexpr int V = CorrT<T>::kVecs;
-    uint4 ra[V], rb[V], rc[V];
+    // register ring of kRing tiles, rotated by NAME (the loop is unrolled by
+    // kRing): while tile i multiplies, tiles i + 1 .. i + kRing - 1 are in
+    // flight and the wait before tile i only drains tile i's own loads.  (A
+    // rotation by register moves forces a full vmcnt(0) drain every tile:
+    // moving the youngest tile's registers waits for its loads.)
+    u32x4 ring[kRing][V];
     {
-      const T* s0 = tile_src(0);
-      const T* s1 = tile_src(1);
-      const T* s2 = tile_src(2);
-      // issue order ra, rb, rc (sched barriers): the wait before the first
-      // tile then drains only ra's loads
+      // issue order slot 0, 1, ... (sched barriers): the wait before the first
+      // tile then drains only slot 0's loads
 #pragma unroll
-      for (int h = 0; h < V; h++) ra[h] = tile_vec(s0, h);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int h = 0; h < V; h++) rb[h] = tile_vec(s1, h);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int h = 0; h < V; h++) rc[h] = tile_vec(s2, h);
+      for (int k = 0; k < kRing; k++) {
+        load_tile(ring[k], k);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
-    auto step = [&](uint4 (&cur)[V], int i) __attribute__((always_inline)) {
+    auto step = [&](u32x4 (&cur)[V], int i) __attribute__((always_inline)) {
+      const bool live = i < nT;  // the last group may hold 1-2 slots past the end
       // two accumulators (even / odd channel groups): two independent MFMA
       // chains, summed once per tile in a fixed order
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      const bool live = i < nT;  // the last group may hold 1-2 slots past the end
-      if (live) {
-      if constexpr (kHalf) {
-        // 8 K steps of 16 channels: vector h holds steps 2h (lo) and 2h + 1 (hi)
+      auto mma = [&](const u32x4 (&B)[V]) __attribute__((always_inline)) {
+        if constexpr (kHalf) {
+          // 8 K steps of 16 channels: vector h holds steps 2h (lo) and 2h + 1 (hi)
 #pragma unroll
-        for (int h = 0; h < V; h++) {
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x16f16(Afh[2 * h], h4_lo(cur[h]), acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x16f16(Afh[2 * h + 1], h4_hi(cur[h]), acc1, 0, 0, 0);
+          for (int h = 0; h < V; h++) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x16f16(Afh[2 * h], h4_lo(B[h]), acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x16f16(Afh[2 * h + 1], h4_hi(B[h]), acc1, 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int h = 0; h < 8; h += 2) {
+            const float4 c0 = __builtin_bit_cast(float4, B[h]);
+            const float4 c1 = __builtin_bit_cast(float4, B[h + 1]);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 0], c0.x, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 4], c1.x, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 1], c0.y, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 5], c1.y, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 2], c0.z, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 6], c1.z, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 3], c0.w, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 7], c1.w, acc1, 0, 0, 0);
+          }
         }
-      } else {
-#pragma unroll
-        for (int h = 0; h < 8; h += 2) {
-          const float4 c0 = __builtin_bit_cast(float4, cur[h]);
-          const float4 c1 = __builtin_bit_cast(float4, cur[h + 1]);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 0], c0.x, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 4], c1.x, acc1, 0, 0, 0);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 1], c0.y, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 5], c1.y, acc1, 0, 0, 0);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 2], c0.z, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 6], c1.z, acc1, 0, 0, 0);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 3], c0.w, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 7], c1.w, acc1, 0, 0, 0);
-        }
-      }
-      }
-      {  // refill this slot with tile i + 3 (past the end: the last tile again, never
-         // used); unconditional, so every path into the next group has the same
-         // load order and the wait before a tile drains only that tile's loads
-        const T* src = tile_src(i + 3);
-#pragma unroll
-        for (int h = 0; h < V; h++) cur[h] = tile_vec(src, h);
+      };
+      if (live) mma(cur);
+      {
+        // refill this slot with tile i + kRing (past the end: the last tile again,
+        // never used); unconditional, so every path into the next group has the
+        // same load order and the wait before a tile drains only that tile's loads
+        load_tile(cur, i + kRing);
       }
       if (!live) return;
       const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
-      const int lb = (j == 0 ? 0 : j == 1 ? cum[1] : j == 2 ? cum[2] : cum[3]);
-      const int t = i - lb, l = level_at(j);
+      const int t = i - pick(j, 0, cum[1], cum[2], cum[3]), l = level_at(j);
       // D: lane holds rows 4q + r (patch pixels), column lane & 15 (box pixel)
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int row = 4 * aq + r;
         if (row < np) G[row * kBoxStride + 16 * t + ai] = acc0[r] + acc1[r];
       }
-      const int le = (j == 0 ? cum[1] : j == 1 ? cum[2] : j == 2 ? cum[3] : cum[4]);
+      const int le = pick(j, cum[1], cum[2], cum[3], cum[4]);
       if (i + 1 == le) {  // level complete: bilinear, then G is free again
         wave_lds_sync();
         CORR_STAMP(2 + 2 * l);
@@ -473,49 +505,21 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     };
     // no early exit inside a group: a break path into the loop's flow block
     // would make the compiler wait for every outstanding load at the top
-    for (int i = 0; i < nT; i += 3) {
-      step(ra, i);
-      step(rb, i + 1);
-      step(rc, i + 2);
+    for (int i = 0; i < nT; i += kRing) {
+#pragma unroll
+      for (int k = 0; k < kRing; k++) step(ring[k], i + k);
     }
   }
 
   // ---- one contiguous [nout][L] row block per edge
   CORR_STAMP(10);
   float* dst = out + ((size_t)b * M + m) * nout * L;
-  if constexpr (RAW9) {
-    if (rx < 7 && ry < 7) {
-      float* d = dst + (size_t)(rx * 7 + ry) * 9 * L;
-#pragma unroll
-      for (int k = 0; k < 9; k++) {
-        if (L == 4) {
-          *reinterpret_cast<float4*>(d + 4 * k) =
-              make_float4(outv[k][0], outv[k][1], outv[k][2], outv[k][3]);
-        } else if (L == 2) {
-          *reinterpret_cast<float2*>(d + 2 * k) = make_float2(outv[k][0], outv[k][1]);
-        } else {
-#pragma unroll
-          for (int ll = 0; ll < kMaxL; ll++)
-            if (ll < L) d[k * L + ll] = outv[k][ll];
-        }
-      }
-    }
+  wave_lds_sync();
+  if (((nout * L) & 3) == 0) {  // whole float4s; the block start is 16-B aligned then too
+    for (int e = 4 * lane; e < nout * L; e += 4 * kWave)
+      *reinterpret_cast<float4*>(dst + e) = *reinterpret_cast<const float4*>(obuf + e);
   } else {
-#pragma unroll
-    for (int u = 0; u < kOutPerLane; u++) {
-      const int o = lane + kWave * u;
-      if (o >= nout) continue;
-      if (L == 4) {
-        *reinterpret_cast<float4*>(dst + (size_t)o * 4) =
-            make_float4(outv[u][0], outv[u][1], outv[u][2], outv[u][3]);
-      } else if (L == 2) {
-        *reinterpret_cast<float2*>(dst + (size_t)o * 2) = make_float2(outv[u][0], outv[u][1]);
-      } else {
-#pragma unroll
-        for (int ll = 0; ll < kMaxL; ll++)
-          if (ll < L) dst[(size_t)o * L + ll] = outv[u][ll];
-      }
-    }
+    for (int e = lane; e < nout * L; e += kWave) dst[e] = obuf[e];
   }
   CORR_STAMP(11);
   CORR_STAMP_RT(13);
@@ -716,7 +720,8 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   const int D = 2 * radius + 2;
   if (D * D > kBoxStride) return DPVO_ERR_UNSUPPORTED;
   const size_t smem = sizeof(float) * kNhwcWaves * np * kBoxStride +
-                      sizeof(NhwcGeom) * kNhwcWaves * kMaxL;
+                      sizeof(NhwcGeom) * kNhwcWaves * kMaxL +
+                      sizeof(float) * kNhwcWaves * corr_obuf_floats(np, radius, L);
   const long long units = (long long)B * M;
   unsigned grid = (unsigned)((units + kNhwcWaves - 1) / kNhwcWaves);
   const bool ordered = order && B == 1;
