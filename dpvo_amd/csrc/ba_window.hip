@@ -145,21 +145,37 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
   }
   __syncthreads();
   int kmin = 0x7fffffff, kmax = -1, fmin = 0x7fffffff, bad = 0;
-  for (int e = tid; e < E; e += T) {
-    int64_t v = kk[e];
-    if (v < 0 || v > kmaxc) {
-      bad = 1;
-      v = v < 0 ? 0 : kmaxc;
+  {
+    // every load of the edge list issued before the first use: ONE global
+    // round trip (a strided loop with the uses inside waits once per pass)
+    constexpr int kPer = kWMaxE / kPT;
+    int64_t vk[kPer], vi[kPer], vj[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const int e = tid + r * T;
+      vk[r] = (e < E) ? kk[e] : 0;
+      vi[r] = (e < E) ? ii[e] : 0;
+      vj[r] = (e < E) ? jj[e] : 0;
     }
-    kmin = min(kmin, (int)v);
-    kmax = max(kmax, (int)v);
-    kkv[e] = (int)v;
-    const int64_t gi = ii[e], gj = jj[e];
-    const bool fi = gi >= t0 && gi < t0 + N, fj = gj >= t0 && gj < t0 + N;
-    const int ci = fi ? (int)(gi - t0) : (int)kFix, cj = fj ? (int)(gj - t0) : (int)kFix;
-    if (!fi) fmin = min(fmin, (int)min(max(gi, (int64_t)0), (int64_t)num_poses - 1));
-    if (!fj) fmin = min(fmin, (int)min(max(gj, (int64_t)0), (int64_t)num_poses - 1));
-    code[e] = (unsigned)ci | ((unsigned)cj << 8);
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const int e = tid + r * T;
+      if (e >= E) continue;
+      int64_t v = vk[r];
+      if (v < 0 || v > kmaxc) {
+        bad = 1;
+        v = v < 0 ? 0 : kmaxc;
+      }
+      kmin = min(kmin, (int)v);
+      kmax = max(kmax, (int)v);
+      kkv[e] = (int)v;
+      const int64_t gi = vi[r], gj = vj[r];
+      const bool fi = gi >= t0 && gi < t0 + N, fj = gj >= t0 && gj < t0 + N;
+      const int ci = fi ? (int)(gi - t0) : (int)kFix, cj = fj ? (int)(gj - t0) : (int)kFix;
+      if (!fi) fmin = min(fmin, (int)min(max(gi, (int64_t)0), (int64_t)num_poses - 1));
+      if (!fj) fmin = min(fmin, (int)min(max(gj, (int64_t)0), (int64_t)num_poses - 1));
+      code[e] = (unsigned)ci | ((unsigned)cj << 8);
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -543,11 +559,27 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   // (#patches << 16 | #edges) (E <= 4096 keeps both below 2^16).
   const unsigned need = (NB > 0) ? ((1u << a) | (1u << b)) : 0u;
   int* cnt = (int*)(lds + off);  // [nuniq] scan input / prefix (kept until the records are built)
-  for (int u = tid; u < nuniq; u += kWT) {
-    const unsigned m = A.plan.pmask[u];
-    const bool rel = (NB == 0) ? true
-                               : (((m & need) == need && (u % S) == sub) || (g == 0 && m == 0));
-    cnt[u] = rel ? ((1 << 16) | (A.plan.poff[u + 1] - A.plan.poff[u])) : 0;
+  // setup loops load kB items per thread before using any (one global round
+  // trip per kB * 256 items instead of one per 256)
+  constexpr int kB = 8;
+  for (int u0 = tid; u0 < nuniq; u0 += kB * kWT) {
+    unsigned m[kB];
+    int p0[kB], p1[kB];
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      const int u = u0 + r * kWT;
+      m[r] = (u < nuniq) ? A.plan.pmask[u] : 0u;
+      p0[r] = (u < nuniq) ? A.plan.poff[u] : 0;
+      p1[r] = (u < nuniq) ? A.plan.poff[u + 1] : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      const int u = u0 + r * kWT;
+      if (u >= nuniq) continue;
+      const bool rel = (NB == 0) ? true
+                                 : (((m[r] & need) == need && (u % S) == sub) || (g == 0 && m[r] == 0));
+      cnt[u] = rel ? ((1 << 16) | (p1[r] - p0[r])) : 0;
+    }
   }
   __syncthreads();
   const int tot = fscan(cnt, nuniq, scr);
@@ -607,51 +639,99 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   }
   // pass A, thread per relevant patch: records, edge offsets, patch of each edge
   int* rpo = reinterpret_cast<int*>(L.qu);  // first sorted position (until the first linearisation)
-  for (int u = tid; u < nuniq && nrel > 0; u += kWT) {
-    const int c0 = cnt[u], c1 = (u + 1 < nuniq) ? cnt[u + 1] : tot;
-    if (c1 == c0) continue;
-    const int ri = c0 >> 16, q0 = c0 & 0xffff, ne = (c1 - c0) & 0xffff;
-    L.roff[ri] = q0;
-    rpo[ri] = A.plan.poff[u];
-    for (int t = 0; t < ne; t++) L.rp[q0 + t] = (unsigned short)ri;
-    if (ne > kChunk) ctl[cCap] = 1;
-    const int kx = A.plan.pkk[u];
-    const float* pk = A.patches + (size_t)kx * 3 * PP;
-    const int c11 = P + 1;  // [*][1][1] (ba_cuda.cu:282-285)
-    const float px = pk[c11], py = pk[PP + c11];
-    L.nxy[ri] = make_float2((px - cx) / fx, (py - cy) / fy);
-    L.dep[ri] = pk[2 * PP + c11];
-    L.dbase[ri] = pk[2 * PP];  // patch_retr_kernel reads [2][0][0] (:225)
-    // writer of the final depth: the diagonal workgroup of the lowest free
-    // pose with share u % Sd; workgroup 0 for patches without a free pose
-    const unsigned m = A.plan.pmask[u];
-    bool own;
-    if (NB == 0) own = true;
-    else if (m == 0) own = (g == 0);
-    else own = diag && (int)__builtin_ctz(m) == a && (u % A.Sd) == sub;
-    L.pkx[ri] = own ? kx : -1;
+  for (int u0 = tid; u0 < nuniq && nrel > 0; u0 += kB * kWT) {
+    int kx[kB], po[kB];
+    unsigned msk[kB];
+    float cv[kB][4];  // [0][1][1], [1][1][1], [2][1][1], [2][0][0] (ba_cuda.cu:282-285, :225)
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      const int u = u0 + r * kWT;
+      const bool live = u < nuniq && cnt[u] != ((u + 1 < nuniq) ? cnt[u + 1] : tot);
+      kx[r] = live ? A.plan.pkk[u] : -1;
+      po[r] = live ? A.plan.poff[u] : 0;
+      msk[r] = live ? A.plan.pmask[u] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      const float* pk = A.patches + (size_t)max(kx[r], 0) * 3 * PP;
+      const int c11 = P + 1;
+      cv[r][0] = (kx[r] >= 0) ? pk[c11] : 0.f;
+      cv[r][1] = (kx[r] >= 0) ? pk[PP + c11] : 0.f;
+      cv[r][2] = (kx[r] >= 0) ? pk[2 * PP + c11] : 0.f;
+      cv[r][3] = (kx[r] >= 0) ? pk[2 * PP] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      if (kx[r] < 0) continue;
+      const int u = u0 + r * kWT;
+      const int c0 = cnt[u], c1 = (u + 1 < nuniq) ? cnt[u + 1] : tot;
+      const int ri = c0 >> 16, q0 = c0 & 0xffff, ne = (c1 - c0) & 0xffff;
+      L.roff[ri] = q0;
+      rpo[ri] = po[r];
+      for (int t = 0; t < ne; t++) L.rp[q0 + t] = (unsigned short)ri;
+      if (ne > kChunk) ctl[cCap] = 1;
+      L.nxy[ri] = make_float2((cv[r][0] - cx) / fx, (cv[r][1] - cy) / fy);
+      L.dep[ri] = cv[r][2];
+      L.dbase[ri] = cv[r][3];  // patch_retr_kernel reads [2][0][0] (:225)
+      // writer of the final depth: the diagonal workgroup of the lowest free
+      // pose with share u % Sd; workgroup 0 for patches without a free pose
+      const unsigned m = msk[r];
+      bool own;
+      if (NB == 0) own = true;
+      else if (m == 0) own = (g == 0);
+      else own = diag && (int)__builtin_ctz(m) == a && (u % A.Sd) == sub;
+      L.pkx[ri] = own ? kx[r] : -1;
+    }
   }
   if (tid == 0) L.roff[nrel] = nrp;
   __syncthreads();
   // pass B, thread per relevant edge: slots, edge index, target/weight
-  for (int q = tid; q < nrp; q += kWT) {
-    const int ri = L.rp[q];
-    const int e = A.plan.epos[rpo[ri] + (q - L.roff[ri])];
-    const unsigned si = wslot((int)A.ii[e], A.t0, N, fmin), sj = wslot((int)A.jj[e], A.t0, N, fmin);
-    L.ec[q] = (unsigned short)(si | (sj << 8));
-    L.eid[q] = e;
-    const float2 tg = reinterpret_cast<const float2*>(A.target)[e];
-    const float2 wt = reinterpret_cast<const float2*>(A.weight)[e];
-    L.tw[q] = make_float4(tg.x, tg.y, wt.x, wt.y);
+  for (int q0 = tid; q0 < nrp; q0 += kB * kWT) {
+    int ev[kB];
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      const int q = q0 + r * kWT;
+      int e = 0;
+      if (q < nrp) {
+        const int ri = L.rp[q];
+        e = A.plan.epos[rpo[ri] + (q - L.roff[ri])];
+      }
+      ev[r] = e;
+    }
+    int64_t gi[kB], gj[kB];
+    float2 tg[kB], wt[kB];
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      const int e = ev[r];
+      gi[r] = A.ii[e];
+      gj[r] = A.jj[e];
+      tg[r] = reinterpret_cast<const float2*>(A.target)[e];
+      wt[r] = reinterpret_cast<const float2*>(A.weight)[e];
+    }
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      const int q = q0 + r * kWT;
+      if (q >= nrp) continue;
+      const unsigned si = wslot((int)gi[r], A.t0, N, fmin), sj = wslot((int)gj[r], A.t0, N, fmin);
+      L.ec[q] = (unsigned short)(si | (sj << 8));
+      L.eid[q] = ev[r];
+      L.tw[q] = make_float4(tg[r].x, tg[r].y, wt[r].x, wt[r].y);
+    }
   }
   // pose table: free poses t0.., then fixed ones from fmin
-  for (int k = tid; k < kWSlots * 8; k += kWT) {
-    const int sl = k >> 3, c = k & 7;
-    const int gp = (sl < N) ? A.t0 + sl : fmin + (sl - N);
-    float v = (c == 6) ? 1.0f : 0.0f;
-    if (c < 7 && gp >= 0 && gp < A.num_poses && (sl < N || fmin != 0x7fffffff))
-      v = A.poses[7 * (size_t)gp + c];
-    L.pose[k] = v;
+  {
+    constexpr int kPr = kWSlots * 8 / kWT;
+    float pv[kPr];
+#pragma unroll
+    for (int r = 0; r < kPr; r++) {
+      const int k = tid + r * kWT, sl = k >> 3, c = k & 7;
+      const int gp = (sl < N) ? A.t0 + sl : fmin + (sl - N);
+      pv[r] = (c == 6) ? 1.0f : 0.0f;
+      if (c < 7 && gp >= 0 && gp < A.num_poses && (sl < N || fmin != 0x7fffffff))
+        pv[r] = A.poses[7 * (size_t)gp + c];
+    }
+#pragma unroll
+    for (int r = 0; r < kPr; r++) L.pose[tid + r * kWT] = pv[r];
   }
   __syncthreads();
   mark(A, 1);
