@@ -175,9 +175,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--no-overlap", action="store_true",
-                    help="run the BA edge grouping inline instead of on a side stream "
-                         "concurrently with A-CORR")
+    ap.add_argument("--overlap", action="store_true",
+                    help="issue the BA edge grouping (fastba.plan) on a side stream "
+                         "concurrently with A-CORR.  Off by default: in the replayed graph the "
+                         "cross-queue join before the BA costs ~11 us, more than the 12 us "
+                         "plan kernel it hides (profiles/r02_trace_overlap_vs_inline.txt)")
     ap.add_argument("--sharded", action="store_true",
                     help="cfg4 global BA, edge-sharded over the ranks (one RCCL all_reduce of "
                          "the packed (S, y) per iteration); --config picks the large graph")
@@ -235,7 +237,7 @@ def main():
     def step(i=0, ev=None):
         cur = torch.cuda.current_stream()
         ws = None
-        if not args.no_overlap:
+        if args.overlap:
             # the BA edge grouping reads the patch graph only (fixed before the
             # update, dpvo.py:775-824): issue it on a side stream so it runs
             # concurrently with the frame insertion / reprojection / A-CORR
@@ -255,7 +257,7 @@ def main():
         corr = altcorr.corr_levels(gbuf, pyr, coords, kk1, jj1, 3, scales, order=order)
         if ev is not None:
             ev[1].record()
-        if not args.no_overlap:
+        if args.overlap:
             cur.wait_stream(plan_stream)
         fastba.BA(poses, patches, D.intrinsics, D.target, D.weight, lmbda, D.ii, D.jj, D.kk, 1,
                   G.F, M=G.M, iterations=args.ba_iters, plan=ws)
@@ -364,7 +366,7 @@ def main():
             "dtype": "f32" if args.features == "f32" else "f16 features, f32 accumulate",
             "data": "synthetic (SURVEY 8d cfg2 recipe, seeded)",
             "launch": "eager" if graph is None else "hipGraph replay of one captured step",
-            "ba_plan": "inline" if args.no_overlap else "side stream, concurrent with A-CORR",
+            "ba_plan": "side stream, concurrent with A-CORR" if args.overlap else "inline (same stream)",
             "config": {
                 "workload": f"{args.config}: {G.M} patches/frame x {G.E} edges, p={P}, "
                             f"{len(levels)}-level pyramid {levels}, "
