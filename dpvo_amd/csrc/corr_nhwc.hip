@@ -159,6 +159,7 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   const bool idx_ok = ix >= 0 && ix < N1 && jx >= 0 && jx < N2;
   const int C = kNhwcC, D = 2 * R + 2, Dp = D - 1, nout = Dp * Dp * np;
   const float cv = (lane < 2 * np) ? coords[((size_t)b * M + m) * 2 * np + lane] : 0.f;
+  __builtin_amdgcn_sched_barrier(0);  // coords first: the geometry then waits for them only
 
   // ---- gmap patch [C][np] -> LDS (in G, free until the first tile) -> A
   // fragments: lane (i = lane & 15, q = lane >> 4) holds f1[c][i] for
@@ -167,22 +168,28 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   constexpr bool kHalf = std::is_same<T, __half>::value;
   float Af[kHalf ? 1 : kNhwcC / 4];
   f16x4 Afh[kHalf ? kNhwcC / 16 : 1];
+  // the patch's loads are issued here; they are staged into the A fragments
+  // only after the first box tiles have been issued (build_A below), so the
+  // gmap round trip and the first tiles' round trip overlap
+  constexpr int kPerA = 16 / sizeof(T);  // 16-B units of the [C][np] patch
+  constexpr int kRA = (kNhwcC * kNpMax / kPerA + kWave - 1) / kWave;
+  const int n16 = (C * np) / kPerA;  // C * np is a multiple of 8 (C = 128)
+  u32x4 st[kRA];
   {
-    // 16-B units of the [C][np] patch (4 floats or 8 halves each)
-    constexpr int kPer = 16 / sizeof(T);
     const T* f1 = fmap1 + ((size_t)b * N1 + (idx_ok ? ix : 0)) * C * np;
-    const int n16 = (C * np) / kPer;  // C * np is a multiple of 8 (C = 128)
-    constexpr int kR = (kNhwcC * kNpMax / kPer + kWave - 1) / kWave;
-    uint4 st[kR];
 #pragma unroll
-    for (int r = 0; r < kR; r++) {
+    for (int r = 0; r < kRA; r++) {
       const int v = lane + kWave * r;
-      st[r] = (v < n16) ? reinterpret_cast<const uint4*>(f1)[v] : make_uint4(0u, 0u, 0u, 0u);
+      // unconditional (clamped) loads: no branch around them, so the waits below
+      // count exactly (a conditional load makes the compiler drain everything)
+      st[r] = reinterpret_cast<const u32x4*>(f1)[min(v, n16 - 1)];
     }
+  }
+  auto build_A = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int r = 0; r < kR; r++) {
+    for (int r = 0; r < kRA; r++) {
       const int v = lane + kWave * r;
-      if (v < n16) reinterpret_cast<uint4*>(G)[v] = st[r];
+      if (v < n16) reinterpret_cast<u32x4*>(G)[v] = st[r];
     }
     wave_lds_sync();
     const bool arow = idx_ok && ai < np;
@@ -202,7 +209,8 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
         for (int s = 0; s < 4; s++)
           Af[4 * h + s] = arow ? G[(16 * h + 4 * aq + s) * np + ai] : 0.0f;
     }
-  }
+    wave_lds_sync();  // A fragments read: G free again
+  };
 
   // ---- geometry of every level up front, lane-parallel: lane (l = lane >> 4,
   // k = lane & 15) takes patch pixel k at level l (floor / frac), 16-lane
@@ -248,7 +256,7 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
       geo[gl].ntile = (bw * bh + 15) >> 4;
     }
   }
-  wave_lds_sync();  // geo visible, A fragments read (G free)
+  wave_lds_sync();  // geo visible
   // Level order: the fine level streams from HBM / the Infinity Cache, the
   // coarse levels hit in L2 and are matrix-core bound.  The second wave on a
   // SIMD (hardware wave slot, HW_ID[3:0]) walks the levels coarse -> fine, so
@@ -357,31 +365,6 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     else bilinear_gen(l, fast);
   };
 
-  // levels off the fast path (empty box, or windows too spread for it) first
-  for (int l = 0; l < L; l++) {
-    const int nt = wave_uniform(geo[l].ntile);
-    if (nt > kMaxTiles) {  // raw[k][yy][xx] directly into G
-      const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
-      const T* f2 = static_cast<const T*>(LV_SEL(f2, l)) + ((size_t)b * N2 + jx) * H2 * W2 * C;
-      for (int e = lane; e < np * D * D; e += kWave) {
-        const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
-        const int i1 = geo[l].y0[k] + yy - R, j1 = geo[l].x0[k] + xx - R;
-        float sacc = 0.f;
-        if (idx_ok && i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
-          const T* px = f2 + ((size_t)i1 * W2 + j1) * C;
-          const T* f1 = fmap1 + ((size_t)b * N1 + ix) * C * np;
-          for (int c = 0; c < C; c++) sacc += to_acc(f1[(size_t)c * np + k]) * to_acc(px[c]);
-        }
-        G[e] = sacc;
-      }
-      wave_lds_sync();
-      bilinear(l, false);
-      wave_lds_sync();
-    } else if (nt == 0) {
-      bilinear(l, true);  // every tap reads 0 (out of the empty box)
-    }
-  }
-
   // ---- flattened fast-path tiles, kRing - 1 in flight
   const int nT = cum[kMaxL];  // == cum[L]: positions >= L add no tiles
   constexpr int V = CorrT<T>::kVecs;  // 16-B loads per lane per tile
@@ -433,22 +416,48 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
         dst[h] = *reinterpret_cast<const u32x4*>(s + (kHalf ? 8 * h : 16 * h));
     }
   };
+  u32x4 ring[kRing][V];
   if (nT > 0) {
     // register ring of kRing tiles, rotated by NAME (the loop is unrolled by
     // kRing): while tile i multiplies, tiles i + 1 .. i + kRing - 1 are in
     // flight and the wait before tile i only drains tile i's own loads.  (A
     // rotation by register moves forces a full vmcnt(0) drain every tile:
     // moving the youngest tile's registers waits for its loads.)
-    u32x4 ring[kRing][V];
-    {
-      // issue order slot 0, 1, ... (sched barriers): the wait before the first
-      // tile then drains only slot 0's loads
+    // issue order slot 0, 1, ... (sched barriers): the wait before the first
+    // tile then drains only slot 0's loads
 #pragma unroll
-      for (int k = 0; k < kRing; k++) {
-        load_tile(ring[k], k);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+    for (int k = 0; k < kRing; k++) {
+      load_tile(ring[k], k);
+      __builtin_amdgcn_sched_barrier(0);
     }
+  }
+  build_A();
+  // levels off the fast path (empty box, or windows too spread for it) first
+  for (int l = 0; l < L; l++) {
+    const int nt = wave_uniform(geo[l].ntile);
+    if (nt > kMaxTiles) {  // raw[k][yy][xx] directly into G
+      const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
+      const T* f2 = static_cast<const T*>(LV_SEL(f2, l)) + ((size_t)b * N2 + jx) * H2 * W2 * C;
+      for (int e = lane; e < np * D * D; e += kWave) {
+        const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
+        const int i1 = geo[l].y0[k] + yy - R, j1 = geo[l].x0[k] + xx - R;
+        float sacc = 0.f;
+        if (idx_ok && i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
+          const T* px = f2 + ((size_t)i1 * W2 + j1) * C;
+          const T* f1 = fmap1 + ((size_t)b * N1 + ix) * C * np;
+          for (int c = 0; c < C; c++) sacc += to_acc(f1[(size_t)c * np + k]) * to_acc(px[c]);
+        }
+        G[e] = sacc;
+      }
+      wave_lds_sync();
+      bilinear(l, false);
+      wave_lds_sync();
+    } else if (nt == 0) {
+      bilinear(l, true);  // every tap reads 0 (out of the empty box)
+    }
+  }
+
+  if (nT > 0) {
     auto step = [&](u32x4 (&cur)[V], int i) __attribute__((always_inline)) {
       const bool live = i < nT;  // the last group may hold 1-2 slots past the end
       // two accumulators (even / odd channel groups): two independent MFMA
