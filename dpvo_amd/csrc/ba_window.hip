@@ -67,13 +67,7 @@ struct Plan {          // written by ba_plan_kernel, read by ba_window_kernel
   int* meta;           // [8] nuniq, fmin, status
   int* status;         // the workspace status word, reset here
   int* sink;           // caller's sticky status word or null
-  int64_t* marks;      // diagnostic shader-clock stamps of thread 0 (may be null)
 };
-
-#define PLAN_MARK(k)                                                          \
-  do {                                                                        \
-    if (plan.marks && tid == 0) plan.marks[k] = (int64_t)__builtin_amdgcn_s_memtime(); \
-  } while (0)
 
 struct WArgs {
   float* poses;
@@ -143,14 +137,13 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
   int* kkv = (int*)(lds + 256 + al16(sizeof(unsigned) * kWMaxE)); // [E] kk (clamped)
   char* big = lds + 256 + 2 * al16(sizeof(unsigned) * kWMaxE);   // sort area
   const int kmaxc = num_patches - 1;
-  PLAN_MARK(0);
   if (tid == 0) {
     ctl[0] = 0x7fffffff;  // kmin
     ctl[1] = -1;          // kmax
     ctl[2] = 0x7fffffff;  // fmin
     ctl[3] = 0;           // status
   }
-  __syncthreads(); PLAN_MARK(1);
+  __syncthreads();
   int kmin = 0x7fffffff, kmax = -1, fmin = 0x7fffffff, bad = 0;
   {
     // every load of the edge list issued before the first use: ONE global
@@ -197,7 +190,7 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
     atomicMin(&ctl[2], fmin);
     if (bad) atomicOr(&ctl[3], kStClamp);
   }
-  __syncthreads(); PLAN_MARK(2);
+  __syncthreads();
   kmin = ctl[0];
   const int R = ctl[1] - kmin + 1;
   int* spos = (int*)big;                 // [E] edge at position p
@@ -206,18 +199,18 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
   if (R <= kHistMax) {
     int* hist = head + kWMaxE;           // [R]
     for (int v = tid; v < R; v += T) hist[v] = 0;
-    __syncthreads(); PLAN_MARK(3);
+    __syncthreads();
     for (int e = tid; e < E; e += T) atomicAdd(&hist[key_of(e)], 1);
-    __syncthreads(); PLAN_MARK(4);
+    __syncthreads();
     fscan(hist, R, scr);                 // hist[v] = first position of bucket v
     for (int p = tid; p < E; p += T) head[p] = 0;
-    __syncthreads(); PLAN_MARK(5);
+    __syncthreads();
     for (int v = tid; v < R; v += T) {
       const int a = hist[v], b = (v + 1 < R) ? hist[v + 1] : E;
       if (b > a) head[a] = 1;
     }
     for (int e = tid; e < E; e += T) spos[atomicAdd(&hist[key_of(e)], 1)] = e;
-    __syncthreads(); PLAN_MARK(6);
+    __syncthreads();
     // deterministic order inside a patch: ascending edge index (buckets are tiny)
     for (int v = tid; v < R; v += T) {
       const int b = hist[v], a = (v == 0) ? 0 : hist[v - 1];
@@ -238,7 +231,7 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
     unsigned long long* keys = (unsigned long long*)(head + kWMaxE);
     for (int i = tid; i < P2; i += T)
       keys[i] = (i < E) ? (((unsigned long long)(unsigned)key_of(i) << 32) | (unsigned)i) : ~0ull;
-    __syncthreads(); PLAN_MARK(7);
+    __syncthreads();
     for (int size = 2; size <= P2; size <<= 1)
       for (int stride = size >> 1; stride > 0; stride >>= 1) {
         for (int i = tid; i < P2 / 2; i += T) {
@@ -251,14 +244,14 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
             keys[hi] = a;
           }
         }
-        __syncthreads(); PLAN_MARK(8);
+        __syncthreads();
       }
     for (int p = tid; p < E; p += T) {
       spos[p] = (int)(keys[p] & 0xffffffffull);
       head[p] = (p == 0 || (keys[p] >> 32) != (keys[p - 1] >> 32)) ? 1 : 0;
     }
   }
-  __syncthreads(); PLAN_MARK(9);
+  __syncthreads();
   // patch index of every position: inclusive scan of the heads
   int* hd = head;
   const int nuniq = fscan(hd, E, scr);   // hd[p] = heads strictly before p
@@ -277,9 +270,9 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
   if (tid == 0) plan.poff[nuniq] = E;
   // free-pose masks: OR over the patch's edges (positions are contiguous)
   unsigned* mask = (unsigned*)(hd + kWMaxE);  // [nuniq] (past the sort keys' first half)
-  __syncthreads(); PLAN_MARK(10);
+  __syncthreads();
   for (int u = tid; u < nuniq; u += T) mask[u] = 0u;
-  __syncthreads(); PLAN_MARK(11);
+  __syncthreads();
   for (int p = tid; p < E; p += T) {
     const int u = ((p + 1 < E) ? hd[p + 1] : nuniq) - 1;
     const unsigned c = code[spos[p]];
@@ -287,7 +280,7 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
     const unsigned m = (ci != kFix ? 1u << ci : 0u) | (cj != kFix ? 1u << cj : 0u);
     if (m) atomicOr(&mask[u], m);
   }
-  __syncthreads(); PLAN_MARK(12);
+  __syncthreads();
   for (int u = tid; u < nuniq; u += T) plan.pmask[u] = mask[u];
   if (tid == 0) {
     plan.meta[0] = nuniq;
@@ -296,7 +289,6 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
     if (ctl[3] && plan.sink) atomicOr(plan.sink, ctl[3]);
     *plan.status = 0;  // this call's status word (ORed by the iteration kernel)
   }
-  PLAN_MARK(31);
 }
 
 // ===========================================================================
@@ -1045,7 +1037,6 @@ static Plan plan_view(char* scratch, int E, int* status) {
   p.meta = (int*)s;
   p.status = status;
   p.sink = sink_for_device();
-  p.marks = nullptr;
   return p;
 }
 
@@ -1062,21 +1053,13 @@ static void set_attrs() {
 
 // edge grouping only (reads ii / jj / kk): may run on another stream than
 // the iterations, e.g. concurrently with A-CORR
-static int ba_window_plan_marked(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E,
-                                 int num_patches, int num_poses, int t0, int t1, char* scratch,
-                                 int* status, int64_t* marks, void* stream) {
+int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
+                   int num_poses, int t0, int t1, char* scratch, int* status, void* stream) {
   set_attrs();
-  Plan plan = plan_view(scratch, E, status);
-  plan.marks = marks;
+  const Plan plan = plan_view(scratch, E, status);
   hipLaunchKernelGGL(ba_plan_kernel, dim3(1), dim3(kPT), kWLds, as_stream(stream), ii, jj, kk, E,
                      num_patches, num_poses, t0, t1 - t0, plan);
   return launch_status();
-}
-
-int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
-                   int num_poses, int t0, int t1, char* scratch, int* status, void* stream) {
-  return ba_window_plan_marked(ii, jj, kk, E, num_patches, num_poses, t0, t1, scratch, status,
-                               nullptr, stream);
 }
 
 int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
@@ -1088,9 +1071,8 @@ int ba_window_launch(float* poses, float* patches, const float* intrinsics, cons
                      const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                      const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
                      int iterations, char* scratch, int* status, int64_t* marks, void* stream) {
-  // diagnostic builds of the call (forward_marks): plan stamps in marks[64..95]
-  const int rc = ba_window_plan_marked(ii, jj, kk, E, num_patches, num_poses, t0, t1, scratch,
-                                       status, marks ? marks + 64 : nullptr, stream);
+  const int rc = ba_window_plan(ii, jj, kk, E, num_patches, num_poses, t0, t1, scratch, status,
+                                stream);
   if (rc) return rc;
   return ba_window_run(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
                        num_poses, num_patches, t0, t1, iterations, scratch, status, marks, stream);

@@ -566,7 +566,10 @@ __global__ void __launch_bounds__(256)
 // 128-B channel runs.  Pool order = torch's avg_pool2d (row-major sum in
 // fp32, then / s^2), so the pooled levels are bit-identical to it.
 // ---------------------------------------------------------------------------
-constexpr int kInsTY = 8, kInsTX = 32, kInsTC = 32;
+// 8 x 16 pixel x 32 channel tiles: 600 workgroups for a 160 x 120 x 128 frame, all
+// resident at once (32 x 8 x 32 tiles gave 300: 1.2 rounds over 256 CUs, the tail
+// round nearly empty)
+constexpr int kInsTY = 8, kInsTX = 16, kInsTC = 32;
 constexpr int kInsCS = kInsTY * kInsTX + 1;  // channel stride (+1: no bank conflicts)
 
 struct InsLevels {
@@ -651,22 +654,24 @@ __global__ void __launch_bounds__(256)
   __shared__ float tile[kInsTC * kInsCS];
   const int tx0 = blockIdx.x * kInsTX, ty0 = blockIdx.y * kInsTY, c0 = blockIdx.z * kInsTC;
   const int tid = threadIdx.x;
-  // load: 32 channels x 8 rows x 32 px, 4 px per load (8 per thread, all issued
-  // before the first LDS store: one HBM latency per tile, not eight)
+  // load: 32 channels x 8 rows x 16 px, 4 px per load (all issued before the
+  // first LDS store: one HBM latency per tile)
+  constexpr int kX4 = kInsTX / 4, kV4 = kInsTC * kInsTY * kX4 / 256;
+  constexpr int kV1 = kInsTC * kInsTY * kInsTX / 256;
   if ((W & 3) == 0) {
-    float4 v[8];
+    float4 v[kV4];
 #pragma unroll
-    for (int r = 0; r < 8; r++) {
-      const int k = tid + 256 * r;  // (c, y, x4) = (k >> 6, (k >> 3) & 7, k & 7)
-      const int c = k >> 6, y = (k >> 3) & 7, x = 4 * (k & 7);
+    for (int r = 0; r < kV4; r++) {
+      const int k = tid + 256 * r;  // (c, y, x4)
+      const int c = k / (kInsTY * kX4), y = (k / kX4) % kInsTY, x = 4 * (k % kX4);
       const int gx = tx0 + x, gy = ty0 + y, gc = c0 + c;
       v[r] = (gx < W && gy < H && gc < C) ? ld4(src + ((size_t)gc * H + gy) * W + gx)
                                           : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int r = 0; r < 8; r++) {
+    for (int r = 0; r < kV4; r++) {
       const int k = tid + 256 * r;
-      const int c = k >> 6, y = (k >> 3) & 7, x = 4 * (k & 7);
+      const int c = k / (kInsTY * kX4), y = (k / kX4) % kInsTY, x = 4 * (k % kX4);
       float* t = tile + c * kInsCS + y * kInsTX + x;
       t[0] = v[r].x;
       t[1] = v[r].y;
@@ -674,18 +679,18 @@ __global__ void __launch_bounds__(256)
       t[3] = v[r].w;
     }
   } else {
-    float v[32];
+    float v[kV1];
 #pragma unroll
-    for (int r = 0; r < 32; r++) {
+    for (int r = 0; r < kV1; r++) {
       const int k = tid + 256 * r;
-      const int x = k & 31, y = (k >> 5) & 7, c = k >> 8;
+      const int x = k % kInsTX, y = (k / kInsTX) % kInsTY, c = k / (kInsTX * kInsTY);
       const int gx = tx0 + x, gy = ty0 + y, gc = c0 + c;
       v[r] = (gx < W && gy < H && gc < C) ? to_acc(src[((size_t)gc * H + gy) * W + gx]) : 0.0f;
     }
 #pragma unroll
-    for (int r = 0; r < 32; r++) {
+    for (int r = 0; r < kV1; r++) {
       const int k = tid + 256 * r;
-      tile[(k >> 8) * kInsCS + ((k >> 5) & 7) * kInsTX + (k & 31)] = v[r];
+      tile[(k / (kInsTX * kInsTY)) * kInsCS + ((k / kInsTX) % kInsTY) * kInsTX + (k % kInsTX)] = v[r];
     }
   }
   __syncthreads();

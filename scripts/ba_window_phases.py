@@ -52,10 +52,6 @@ for rep in range(40):
         d[f"it{it}: solve"] = (m[mb + 3] - m[mb + 2]) * 0.01
         prev = mb + 3
     d["final apply + write-back"] = (m[63] - m[prev]) * 0.01
-    # plan kernel: shader-clock stamps of thread 0 after each barrier (m[64 + k])
-    pk = [k for k in range(32) if m[64 + k]]
-    for a_, b_ in zip(pk, pk[1:]):
-        d[f"plan {a_:2d}->{b_:2d} (cycles)"] = m[64 + b_] - m[64 + a_]
     for k, v in d.items():
         acc.setdefault(k, []).append(v)
 print(f"{arg}: E={G.E} N={t1 - t0} iterations={iters}")
