@@ -211,19 +211,18 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
     }
     for (int e = tid; e < E; e += T) spos[atomicAdd(&hist[key_of(e)], 1)] = e;
     __syncthreads();
-    // deterministic order inside a patch: ascending edge index (buckets are tiny)
-    for (int v = tid; v < R; v += T) {
-      const int b = hist[v], a = (v == 0) ? 0 : hist[v - 1];
-      for (int t = a + 1; t < b; t++) {
-        const int x = spos[t];
-        int s2 = t - 1;
-        while (s2 >= a && spos[s2] > x) {
-          spos[s2 + 1] = spos[s2];
-          s2--;
-        }
-        spos[s2 + 1] = x;
-      }
+    // deterministic order inside a patch (ascending edge index): every edge
+    // counts the smaller edges of its bucket, all edges in parallel (was a
+    // serial insertion sort per bucket: a chain of dependent LDS accesses)
+    int* ranked = hist + kHistMax;  // [E]
+    for (int e = tid; e < E; e += T) {
+      const int v = key_of(e);
+      const int b = hist[v], a = (v == 0) ? 0 : hist[v - 1];  // hist[v]: end of bucket v now
+      int rank = 0;
+      for (int t = a; t < b; t++) rank += (spos[t] < e) ? 1 : 0;
+      ranked[a + rank] = e;
     }
+    spos = ranked;
   } else {
     // wide kk range: bitonic sort of (key << 32 | e) over the next power of two
     int P2 = 1;
