@@ -7,8 +7,9 @@ One step = one DPVO update iteration with all inputs resident in HBM:
   F-REPROJ  (cuda_ba.reproject, E x 9 points)
   A-CORR    (all 4 levels in one launch, cuda_corr.forward_levels)
   F-BA      (cuda_ba.forward, 2 iterations, poses/patches updated in place)
-By default the step is captured once as a hipGraph and replayed (--eager:
-launch from Python every step).
+By default every kernel is launched from Python each step, as DPVO runs; the
+host stays ahead of the GPU (--graph: capture the step once as a hipGraph and
+replay it; each replay leaves a ~8.7 us launch gap).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -186,9 +187,11 @@ def main():
     ap.add_argument("--features", choices=["f32", "f16"], default="f32",
                     help="feature dtype of the pyramid / gmap rings (f16 = the fork's "
                          "MIXED_PRECISION runtime: A-CORR on v_mfma_f32_16x16x16_f16)")
-    ap.add_argument("--eager", action="store_true",
-                    help="launch every kernel from Python each step (default: replay the "
-                         "step as one captured hipGraph)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as one captured hipGraph (default: launch every kernel "
+                         "from Python each step, as DPVO does; the host stays ahead of the GPU, "
+                         "while a graph replay leaves a ~8.7 us gap between steps: "
+                         "profiles/r02_trace_overlap_vs_inline.txt)")
     args = ap.parse_args()
 
     import torch
@@ -281,7 +284,7 @@ def main():
         feat_bytes)
 
     graph = None
-    if not args.eager:
+    if args.graph:
         # one update iteration (frame insertion, reproject, corr, 2 BA iterations)
         # captured once and replayed: the same kernels with the same work, without
         # the per-launch Python / runtime gaps
