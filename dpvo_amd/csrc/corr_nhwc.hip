@@ -262,7 +262,11 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   // SIMD (hardware wave slot, HW_ID[3:0]) walks the levels coarse -> fine, so
   // the two waves of a SIMD are in opposite phases instead of both waiting on
   // memory first and both multiplying later.
+#ifdef CORR_NO_REV  // diagnostic builds (scripts/micro/corr_bench): every wave fine -> coarse
+  const bool rev = false;
+#else
   const bool rev = (__builtin_amdgcn_s_getreg((3 << 11) | 4) & 1) != 0;
+#endif
   auto level_at = [&](int j) { return rev ? L - 1 - j : j; };  // position -> level
   cum[0] = 0;
 #pragma unroll
@@ -299,26 +303,38 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     const int xlo = wave_uniform(gg->xlo), ylo = wave_uniform(gg->ylo);
     const int bw = wave_uniform(gg->bw), bh = wave_uniform(gg->bh);
     const int cap = max(bw * bh - 1, 0);
+    // every LDS read of the level first, the obuf writes last: a write between
+    // them (possible alias for the compiler) would serialise the 9 patch pixels
+    float r[9], dxv[9], dyv[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) {
-      float r;
+      dxv[k] = gg->dx[k];
+      dyv[k] = gg->dy[k];
       if (fast) {
         const int gy = gg->y0[k] + ry - R - ylo, gx = gg->x0[k] + rx - R - xlo;
         const bool in = gy >= 0 && gy < bh && gx >= 0 && gx < bw;
         const float a = G[k * kBoxStride + min(max(gy * bw + gx, 0), cap)];
-        r = in ? a : 0.f;
+        r[k] = in ? a : 0.f;
       } else {
-        r = G[k * 64 + ry * 8 + rx];
+        r[k] = G[k * 64 + ry * 8 + rx];
       }
-      const float r10 = __shfl_down(r, 1, kWave);   // (y + 1, x)
-      const float r01 = __shfl_down(r, 8, kWave);   // (y, x + 1)
-      const float r11 = __shfl_down(r, 9, kWave);   // (y + 1, x + 1)
-      const float dx = gg->dx[k], dy = gg->dy[k];
-      float v = ((1.f - dx) * (1.f - dy)) * r;
-      v = v + (dx * (1.f - dy)) * r01;
-      v = v + ((1.f - dx) * dy) * r10;
-      v = v + (dx * dy) * r11;
-      if (rx < 7 && ry < 7) obuf[((rx * 7 + ry) * 9 + k) * L + l] = v;
+    }
+    float v[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      const float r10 = __shfl_down(r[k], 1, kWave);   // (y + 1, x)
+      const float r01 = __shfl_down(r[k], 8, kWave);   // (y, x + 1)
+      const float r11 = __shfl_down(r[k], 9, kWave);   // (y + 1, x + 1)
+      const float dx = dxv[k], dy = dyv[k];
+      float t = ((1.f - dx) * (1.f - dy)) * r[k];
+      t = t + (dx * (1.f - dy)) * r01;
+      t = t + ((1.f - dx) * dy) * r10;
+      t = t + (dx * dy) * r11;
+      v[k] = t;
+    }
+    if (rx < 7 && ry < 7) {
+#pragma unroll
+      for (int k = 0; k < 9; k++) obuf[((rx * 7 + ry) * 9 + k) * L + l] = v[k];
     }
   };
   auto bilinear_gen = [&](int l, bool fast) __attribute__((always_inline)) {
@@ -326,6 +342,7 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     const int xlo = wave_uniform(gg->xlo), ylo = wave_uniform(gg->ylo);
     const int bw = wave_uniform(gg->bw), bh = wave_uniform(gg->bh);
     const int cap = max(bw * bh - 1, 0);
+    float vout[kOuts];
 #pragma unroll
     for (int u = 0; u < kOuts; u++) {
       const int cd = max(code[RAW9 ? 0 : u], 0);
@@ -357,8 +374,12 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
       v = v + (dx * (1.f - dy)) * r01;
       v = v + ((1.f - dx) * dy) * r10;
       v = v + (dx * dy) * r11;
-      if (code[RAW9 ? 0 : u] >= 0) obuf[(lane + kWave * u) * L + l] = v;
+      vout[u] = v;
     }
+    // writes after every read (see bilinear_raw)
+#pragma unroll
+    for (int u = 0; u < kOuts; u++)
+      if (code[RAW9 ? 0 : u] >= 0) obuf[(lane + kWave * u) * L + l] = vout[u];
   };
   auto bilinear = [&](int l, bool fast) __attribute__((always_inline)) {
     if constexpr (RAW9) bilinear_raw(l, fast);

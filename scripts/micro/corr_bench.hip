@@ -37,7 +37,7 @@ __device__ int64_t* g_stamps;  // [edges][16]
 
 int main(int argc, char** argv) {
   const int ordered = argc > 1 ? atoi(argv[1]) : 1;
-  const int F = 12, Mp = 96, E = 2048, mem = 36, C = 128, P = 3, L = 4, R = 3;
+  const int F = 12, Mp = 96, E = argc > 4 ? atoi(argv[4]) : 2048, mem = 36, C = 128, P = 3, L = 4, R = 3;
   const int H = 120, W = 160, scales[4] = {1, 2, 4, 8};
   std::mt19937 rng(0);
   std::uniform_real_distribution<float> U(0.f, 1.f);
