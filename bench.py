@@ -181,6 +181,9 @@ def main():
                          "concurrently with A-CORR.  Off by default: in the replayed graph the "
                          "cross-queue join before the BA costs ~11 us, more than the 12 us "
                          "plan kernel it hides (profiles/r02_trace_overlap_vs_inline.txt)")
+    ap.add_argument("--separate-plan", action="store_true",
+                    help="launch the BA edge grouping as its own kernel after A-CORR (default: "
+                         "inside the reprojection launch, fastba.reproject(plan_window=...))")
     ap.add_argument("--sharded", action="store_true",
                     help="cfg4 global BA, edge-sharded over the ranks (one RCCL all_reduce of "
                          "the packed (S, y) per iteration); --config picks the large graph")
@@ -236,6 +239,8 @@ def main():
     scales = [float(s) for s in levels]
 
     plan_stream = torch.cuda.Stream()
+    fused_plan = (not args.overlap and not args.separate_plan
+                  and fastba.cuda_ba.plan_supported(int(D.ii.numel()), 1, G.F, P))
 
     def step(i=0, ev=None):
         cur = torch.cuda.current_stream()
@@ -253,8 +258,14 @@ def main():
         altcorr.insert_frame(pyr_nchw[0][0, slot], pyr, slot, levels)
         # reprojection + the XCD-aware edge order (edges grouped by target
         # frame) in one launch; A-CORR processes each group on one XCD
-        coords, order = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk,
-                                         mem=args.mem)
+        if fused_plan:
+            # ... and the BA edge grouping (reads ii / jj / kk only, fixed for
+            # the update) as workgroup 0 of the same launch
+            coords, order, ws = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk,
+                                                 mem=args.mem, plan_window=(1, G.F))
+        else:
+            coords, order = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk,
+                                             mem=args.mem)
         if ev is not None:
             ev[0].record()
         corr = altcorr.corr_levels(gbuf, pyr, coords, kk1, jj1, 3, scales, order=order)
@@ -369,7 +380,8 @@ def main():
             "dtype": "f32" if args.features == "f32" else "f16 features, f32 accumulate",
             "data": "synthetic (SURVEY 8d cfg2 recipe, seeded)",
             "launch": "eager" if graph is None else "hipGraph replay of one captured step",
-            "ba_plan": "side stream, concurrent with A-CORR" if args.overlap else "inline (same stream)",
+            "ba_plan": ("side stream, concurrent with A-CORR" if args.overlap else
+                        "in the reprojection launch" if fused_plan else "inline (same stream)"),
             "config": {
                 "workload": f"{args.config}: {G.M} patches/frame x {G.E} edges, p={P}, "
                             f"{len(levels)}-level pyramid {levels}, "

@@ -440,26 +440,8 @@ __global__ void reproject_kernel(const float* __restrict__ poses, const float* _
   const int PP = P * P;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= E * PP) return;
-  const int n = t / PP, pix = t % PP;
-  const float fx = intrinsics[0], fy = intrinsics[1], cx = intrinsics[2], cy = intrinsics[3];
-  const int ix = (int)min(max(ii[n], (int64_t)0), (int64_t)num_poses - 1);
-  const int jx = (int)min(max(jj[n], (int64_t)0), (int64_t)num_poses - 1);
-  const int64_t kx = min(max(kk[n], (int64_t)0), (int64_t)num_patches - 1);
-  const float* pi = poses + 7 * (size_t)ix;
-  const float* pj = poses + 7 * (size_t)jx;
-  float ti[3] = {pi[0], pi[1], pi[2]}, qi[4] = {pi[3], pi[4], pi[5], pi[6]};
-  float tj[3] = {pj[0], pj[1], pj[2]}, qj[4] = {pj[3], pj[4], pj[5], pj[6]};
-  float tij[3], qij[4];
-  relSE3(ti, qi, tj, qj, tij, qij);
-  const float* pk = patches + (size_t)kx * 3 * PP;
-  float Xi[4], Xj[4];
-  Xi[0] = (pk[pix] - cx) / fx;
-  Xi[1] = (pk[PP + pix] - cy) / fy;
-  Xi[2] = 1.0f;
-  Xi[3] = pk[2 * PP + pix];
-  actSE3(tij, qij, Xi, Xj);
-  coords[((size_t)n * 2 + 0) * PP + pix] = fx * (Xj[0] / Xj[2]) + cx;
-  coords[((size_t)n * 2 + 1) * PP + pix] = fy * (Xj[1] / Xj[2]) + cy;
+  reproject_pixel(poses, patches, intrinsics, ii, jj, kk, t / PP, t % PP, P, num_poses,
+                  num_patches, coords);
 }
 #pragma clang fp contract(fast)
 
@@ -1072,6 +1054,10 @@ int ba_window_launch(float* poses, float* patches, const float* intrinsics, cons
                      int iterations, char* scratch, int* status, int64_t* marks, void* stream);
 int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
                    int num_poses, int t0, int t1, char* scratch, int* status, void* stream);
+int ba_window_reproject_plan(const float* poses, const float* patches, const float* intrinsics,
+                             const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int P,
+                             int num_poses, int num_patches, int N2, float* coords, int* order,
+                             int t0, int t1, char* scratch, int* status, void* stream);
 int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
                   const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                   const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
@@ -1408,6 +1394,25 @@ DPVO_EXPORT int dpvo_reproject_ordered(const float* poses, const float* patches,
                      as_stream(stream), poses, patches, intrinsics, ii, jj, kk, E, P, num_poses,
                      num_patches, coords, (int*)order, N2);
   return launch_status();
+}
+
+DPVO_EXPORT int dpvo_reproject_ordered_plan(const float* poses, const float* patches,
+                                            const float* intrinsics, const int64_t* ii,
+                                            const int64_t* jj, const int64_t* kk, int E, int P,
+                                            int num_poses, int num_patches, int N2, float* coords,
+                                            int32_t* order, int t0, int t1, void* workspace,
+                                            size_t workspace_bytes, void* stream) {
+  if (E <= 0) return DPVO_OK;
+  if (P <= 0 || num_poses <= 0 || num_patches <= 0 || !order || !coords || !poses || !patches ||
+      !intrinsics || !ii || !jj || !kk || !workspace || t1 < t0)
+    return DPVO_ERR_INVALID;
+  if (!ba_window_supported(E, t1 - t0, P)) return DPVO_ERR_UNSUPPORTED;
+  if (workspace_bytes < dpvo_ba_workspace_bytes(E, t0, t1)) return DPVO_ERR_WORKSPACE;
+  BaWs w;
+  const size_t base_bytes = ba_layout(E, t1 - t0, (char*)workspace, &w);
+  return ba_window_reproject_plan(poses, patches, intrinsics, ii, jj, kk, E, P, num_poses,
+                                  num_patches, N2, coords, (int*)order, t0, t1,
+                                  (char*)workspace + base_bytes, w.meta + 1, stream);
 }
 
 DPVO_EXPORT int dpvo_neighbors_max_edges(void) { return 1 << 30; }

@@ -124,12 +124,11 @@ __device__ __forceinline__ void wg_block(const WArgs& A, int g, int& a, int& b, 
 // ===========================================================================
 // plan: group edges by patch (one workgroup, 512 threads)
 // ===========================================================================
-__global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict__ ii,
-                                                      const int64_t* __restrict__ jj,
-                                                      const int64_t* __restrict__ kk, int E,
-                                                      int num_patches, int num_poses, int t0, int N,
-                                                      Plan plan) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
+__device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
+                                           const int64_t* __restrict__ jj,
+                                           const int64_t* __restrict__ kk, int E, int num_patches,
+                                           int num_poses, int t0, int N, const Plan& plan,
+                                           char* lds) {
   const int tid = threadIdx.x, lane = tid & 63, T = kPT;
   int* ctl = (int*)lds;                  // [64]
   int* scr = ctl + 16;                   // scan scratch [>= 17]
@@ -288,6 +287,49 @@ __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict_
     if (ctl[3] && plan.sink) atomicOr(plan.sink, ctl[3]);
     *plan.status = 0;  // this call's status word (ORed by the iteration kernel)
   }
+}
+
+__global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict__ ii,
+                                                      const int64_t* __restrict__ jj,
+                                                      const int64_t* __restrict__ kk, int E,
+                                                      int num_patches, int num_poses, int t0, int N,
+                                                      Plan plan) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  plan_block(ii, jj, kk, E, num_patches, num_poses, t0, N, plan, lds);
+}
+
+// One launch for the start of a DPVO update (dpvo.py:775-824): F-REPROJ of
+// every (edge, pixel), the A-CORR edge order and the BA plan.  The plan only
+// reads ii / jj / kk, which the update does not change before its BA, so its
+// single workgroup (the longest, dispatched first as workgroup 0) runs beside
+// the reprojection instead of after A-CORR.
+struct RArgs {
+  const float* poses;
+  const float* patches;
+  const float* intrinsics;
+  const int64_t* ii;
+  const int64_t* jj;
+  const int64_t* kk;
+  int E, P, num_poses, num_patches, N2, t0, N;
+  float* coords;
+  int* order;
+};
+
+__global__ void __launch_bounds__(kPT) reproject_plan_kernel(RArgs R, Plan plan) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  if (blockIdx.x == 0) {
+    plan_block(R.ii, R.jj, R.kk, R.E, R.num_patches, R.num_poses, R.t0, R.N, plan, lds);
+    return;
+  }
+  if (blockIdx.x == 1) {
+    edge_order_block(R.jj, R.E, R.N2, R.order, reinterpret_cast<int*>(lds));
+    return;
+  }
+  const int PP = R.P * R.P;
+  const int t = (blockIdx.x - 2) * kPT + threadIdx.x;
+  if (t >= R.E * PP) return;
+  reproject_pixel(R.poses, R.patches, R.intrinsics, R.ii, R.jj, R.kk, t / PP, t % PP, R.P,
+                  R.num_poses, R.num_patches, R.coords);
 }
 
 // ===========================================================================
@@ -1046,6 +1088,8 @@ static void set_attrs() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
     (void)hipFuncSetAttribute((const void*)ba_plan_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
+    (void)hipFuncSetAttribute((const void*)reproject_plan_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
     attr = true;
   }
 }
@@ -1058,6 +1102,36 @@ int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int 
   const Plan plan = plan_view(scratch, E, status);
   hipLaunchKernelGGL(ba_plan_kernel, dim3(1), dim3(kPT), kWLds, as_stream(stream), ii, jj, kk, E,
                      num_patches, num_poses, t0, t1 - t0, plan);
+  return launch_status();
+}
+
+// reprojection + A-CORR edge order + edge grouping in one launch (shapes
+// validated by the caller, dpvo_reproject_ordered_plan)
+int ba_window_reproject_plan(const float* poses, const float* patches, const float* intrinsics,
+                             const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int P,
+                             int num_poses, int num_patches, int N2, float* coords, int* order,
+                             int t0, int t1, char* scratch, int* status, void* stream) {
+  set_attrs();
+  const Plan plan = plan_view(scratch, E, status);
+  RArgs r;
+  r.poses = poses;
+  r.patches = patches;
+  r.intrinsics = intrinsics;
+  r.ii = ii;
+  r.jj = jj;
+  r.kk = kk;
+  r.E = E;
+  r.P = P;
+  r.num_poses = num_poses;
+  r.num_patches = num_patches;
+  r.N2 = N2;
+  r.t0 = t0;
+  r.N = t1 - t0;
+  r.coords = coords;
+  r.order = order;
+  const int total = E * P * P;
+  hipLaunchKernelGGL(reproject_plan_kernel, dim3(2 + (total + kPT - 1) / kPT), dim3(kPT), kWLds,
+                     as_stream(stream), r, plan);
   return launch_status();
 }
 

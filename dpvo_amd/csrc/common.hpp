@@ -224,6 +224,39 @@ __device__ __forceinline__ void retrSE3(const float* xi, const float* t, const f
   t1[2] += dt[2];
 }
 
+// F-REPROJ of one (edge n, patch pixel pix) (ba_cuda.cu:379-429): shared by
+// reproject_kernel (ba.hip) and the fused reproject + BA-plan launch
+// (ba_window.hip), so both round identically.
+__device__ __forceinline__ void reproject_pixel(const float* __restrict__ poses,
+                                                const float* __restrict__ patches,
+                                                const float* __restrict__ intrinsics,
+                                                const int64_t* __restrict__ ii,
+                                                const int64_t* __restrict__ jj,
+                                                const int64_t* __restrict__ kk, int n, int pix,
+                                                int P, int num_poses, int num_patches,
+                                                float* __restrict__ coords) {
+  const int PP = P * P;
+  const float fx = intrinsics[0], fy = intrinsics[1], cx = intrinsics[2], cy = intrinsics[3];
+  const int ix = (int)min(max(ii[n], (int64_t)0), (int64_t)num_poses - 1);
+  const int jx = (int)min(max(jj[n], (int64_t)0), (int64_t)num_poses - 1);
+  const int64_t kx = min(max(kk[n], (int64_t)0), (int64_t)num_patches - 1);
+  const float* pi = poses + 7 * (size_t)ix;
+  const float* pj = poses + 7 * (size_t)jx;
+  float ti[3] = {pi[0], pi[1], pi[2]}, qi[4] = {pi[3], pi[4], pi[5], pi[6]};
+  float tj[3] = {pj[0], pj[1], pj[2]}, qj[4] = {pj[3], pj[4], pj[5], pj[6]};
+  float tij[3], qij[4];
+  relSE3(ti, qi, tj, qj, tij, qij);
+  const float* pk = patches + (size_t)kx * 3 * PP;
+  float Xi[4], Xj[4];
+  Xi[0] = (pk[pix] - cx) / fx;
+  Xi[1] = (pk[PP + pix] - cy) / fy;
+  Xi[2] = 1.0f;
+  Xi[3] = pk[2 * PP + pix];
+  actSE3(tij, qij, Xi, Xj);
+  coords[((size_t)n * 2 + 0) * PP + pix] = fx * (Xj[0] / Xj[2]) + cx;
+  coords[((size_t)n * 2 + 1) * PP + pix] = fy * (Xj[1] / Xj[2]) + cy;
+}
+
 #pragma clang fp contract(fast)
 
 }  // namespace dpvo

@@ -317,6 +317,34 @@ std::vector<torch::Tensor> ba_reproject_ordered(torch::Tensor poses, torch::Tens
   return {coords.view({1, E, 2, P, P}), order};
 }
 
+// reproject + edge order + BA plan (workspace for forward_planned) in one launch
+std::vector<torch::Tensor> ba_reproject_ordered_plan(torch::Tensor poses, torch::Tensor patches,
+                                                     torch::Tensor intrinsics, torch::Tensor ii,
+                                                     torch::Tensor jj, torch::Tensor kk, int N2,
+                                                     int t0, int t1) {
+  poses = f32_contig(poses, "poses");
+  patches = f32_contig(patches, "patches");
+  intrinsics = f32_contig(intrinsics, "intrinsics");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  kk = idx64(kk, "kk");
+  const int P = patches.size(-1);
+  const int E = ii.numel();
+  TORCH_CHECK(jj.numel() == E && kk.numel() == E, "ii, jj, kk must have equal length");
+  auto coords = torch::empty({E, 2, P, P}, poses.options());
+  auto order = torch::empty({E}, poses.options().dtype(torch::kInt32));
+  const size_t wsb = dpvo_ba_workspace_bytes(E, t0, t1);
+  auto ws = torch::empty({(int64_t)wsb}, poses.options().dtype(torch::kUInt8));
+  check_status(dpvo_reproject_ordered_plan(
+                   poses.data_ptr<float>(), patches.data_ptr<float>(), intrinsics.data_ptr<float>(),
+                   ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), kk.data_ptr<int64_t>(), E, P,
+                   poses.numel() / 7, patches.numel() / (3 * P * P), N2, coords.data_ptr<float>(),
+                   order.data_ptr<int32_t>(), t0, t1, ws.data_ptr(), wsb, current_stream()),
+               "cuda_ba.reproject_ordered_plan");
+  return {coords.view({1, E, 2, P, P}), order, ws};
+}
+
 // ba.cpp:59-97 (host loop in the reference; here one O(E^2) LDS-tiled kernel)
 std::vector<torch::Tensor> ba_neighbors(torch::Tensor ii, torch::Tensor jj) {
   ii = idx64(ii, "ii");
@@ -644,6 +672,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gba_solve_update", &gba_solve_update, "large-graph BA: solve + retraction");
   m.def("gba_info", &gba_info, "status, nuniq, nitems, nblk, nI, nB, g, nsb (device int32[8])");
   m.def("forward_marks", &ba_forward_marks, "forward + per-phase wall-clock marks");
+  m.def("reproject_ordered_plan", &ba_reproject_ordered_plan,
+        "reproject + A-CORR edge order + BA plan (workspace for forward_planned), one launch");
   m.def("reproject_ordered", &ba_reproject_ordered,
         "reproject + edge order by target frame (for cuda_corr.forward_levels(order=))");
   m.def("select_path", [](int mode) { check_status(dpvo_ba_select_path(mode), "select_path"); },

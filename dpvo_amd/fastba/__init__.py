@@ -47,13 +47,23 @@ def neighbors(ii, jj):
     return cuda_ba.neighbors(ii, jj)
 
 
-def reproject(poses, patches, intrinsics, ii, jj, kk, mem=None):
+def reproject(poses, patches, intrinsics, ii, jj, kk, mem=None, plan_window=None):
     """cuda_ba.reproject (ba_cuda.cu:379-429, 585-616).  With ``mem`` (the
     feature ring size the targets jj index), also returns the A-CORR edge
     order (int32 [E], edges grouped by target frame) computed in the same
-    launch: ``coords, order = reproject(..., mem=36)``."""
+    launch: ``coords, order = reproject(..., mem=36)``.  With ``mem`` and
+    ``plan_window=(t0, t1)`` the same launch also groups the edges for the
+    update's BA: ``coords, order, ws = reproject(..., mem=36, plan_window=(t0, t1))``
+    and later ``BA(..., plan=ws)`` (identical to :func:`plan`; the window path
+    must cover the shape, see :func:`plan`)."""
     if mem is None:
+        if plan_window is not None:
+            raise ValueError("reproject: plan_window needs mem")
         return cuda_ba.reproject(poses, patches, intrinsics, ii, jj, kk)
+    if plan_window is not None:
+        t0, t1 = plan_window
+        return tuple(cuda_ba.reproject_ordered_plan(poses, patches, intrinsics, ii, jj, kk,
+                                                    int(mem), int(t0), int(t1)))
     return tuple(cuda_ba.reproject_ordered(poses, patches, intrinsics, ii, jj, kk, int(mem)))
 
 

@@ -127,8 +127,16 @@ class UpdateHarness:
         sync()
         t.append(time.perf_counter())
         ii, jj, kk = self.pg.ii[:E], self.pg.jj[:E], self.pg.kk[:E]
-        coords, order = fastba.reproject(self.poses, self.patches, self.intrinsics, ii, jj, kk,
-                                         mem=self.mem)
+        t0 = max(self.n - self.ow, 1)
+        ws = None
+        if fastba.cuda_ba.plan_supported(E, t0, self.n, self.P):
+            # the BA's edge grouping rides in the reprojection launch (the
+            # edges stay fixed until the BA below)
+            coords, order, ws = fastba.reproject(self.poses, self.patches, self.intrinsics, ii,
+                                                 jj, kk, mem=self.mem, plan_window=(t0, self.n))
+        else:
+            coords, order = fastba.reproject(self.poses, self.patches, self.intrinsics, ii, jj,
+                                             kk, mem=self.mem)
         corr = altcorr.corr_levels(self.gmap, self.pyr, coords, kk % (self.M * self.pmem),
                                    jj % self.mem, 3, self.levels, order=order)
         delta, weight = self._network(coords, ii, jj, kk)
@@ -137,10 +145,9 @@ class UpdateHarness:
         self.pg.weight[0, :E] = weight[0]
         sync()
         t.append(time.perf_counter())
-        t0 = max(self.n - self.ow, 1)
         fastba.BA(self.poses, self.patches, self.intrinsics, self.pg.target[:, :E],
                   self.pg.weight[:, :E], self.lmbda, ii, jj, kk, t0, self.n, M=self.M,
-                  iterations=self.ba_iters)
+                  iterations=self.ba_iters, plan=ws)
         sync()
         t.append(time.perf_counter())
         self.pg.remove_by_window(self.ix, self.n, self.rw)

@@ -308,6 +308,18 @@ int dpvo_reproject_ordered(const float* poses, const float* patches, const float
                            int num_poses, int num_patches, int N2, float* coords, int32_t* order,
                            void* stream);
 
+/* dpvo_reproject_ordered plus dpvo_ba_plan(ii, jj, kk, .., t0, t1, workspace)
+   in the same launch: the start of a DPVO update (dpvo.py:775-824 reprojects,
+   then runs BA on the same edges), so the edge grouping the window BA needs
+   runs beside the reprojection instead of as its own launch.  workspace is
+   then passed to dpvo_ba_forward_planned.  Same outputs, bit for bit, as the
+   two separate calls; DPVO_ERR_UNSUPPORTED where dpvo_ba_plan_supported is 0. */
+int dpvo_reproject_ordered_plan(const float* poses, const float* patches,
+                                const float* intrinsics, const int64_t* ii, const int64_t* jj,
+                                const int64_t* kk, int E, int P, int num_poses, int num_patches,
+                                int N2, float* coords, int32_t* order, int t0, int t1,
+                                void* workspace, size_t workspace_bytes, void* stream);
+
 /* F-NBR.  Replaces cuda_ba.neighbors (ba.cpp:59-97).  Groups edges by ii,
    stable-sorts each group by jj; ix = previous edge, jx = next edge, -1 at
    the ends.  Single-workgroup LDS sort: E <= dpvo_neighbors_max_edges(). */

@@ -76,6 +76,52 @@ def test_planned_forward_is_bit_identical(cb, gpu, cfg):
     assert cb.check_status(poses) == 0
 
 
+@pytest.mark.parametrize("cfg", ["cfg1", "cfg2", "dpvo10"])
+def test_reproject_plan_fused_is_bit_identical(cb, gpu, cfg):
+    """reproject(mem=, plan_window=) (dpvo_reproject_ordered_plan: reprojection,
+    A-CORR edge order and BA plan in one launch) == reproject_ordered + plan:
+    same coords bits, a valid grouping by target frame, and BA(plan=ws) ==
+    BA() bit for bit."""
+    from dpvo_amd import fastba
+
+    if cfg == "dpvo10":  # E = 3940: DPVO's edge pattern inside the window path's E <= 4096
+        G = synthetic.make_dpvo_window(M=10, seed=10)
+        t0, t1 = G.F - 10, G.F
+    else:
+        G = synthetic.make_config(cfg, seed=11)
+        t0, t1 = 1, G.F
+    D = G.to(gpu)
+    lm = torch.tensor([1e-4], device=gpu)
+    mem = int(D.jj.max().item()) + 1
+    c_ref, o_ref = fastba.reproject(D.poses, D.patches, D.intrinsics, D.ii, D.jj, D.kk, mem=mem)
+    c, o, ws = fastba.reproject(D.poses, D.patches, D.intrinsics, D.ii, D.jj, D.kk, mem=mem,
+                                plan_window=(t0, t1))
+    assert torch.equal(c, c_ref)
+    # order: a permutation of the edges, grouped by ascending target frame
+    assert torch.equal(torch.sort(o.long())[0], torch.arange(D.ii.numel(), device=gpu))
+    assert bool((torch.diff(D.jj[o.long()]) >= 0).all())
+    assert torch.equal(torch.sort(D.jj[o.long()])[0], torch.sort(D.jj[o_ref.long()])[0])
+    P0, K0 = _run(cb, G, gpu, t0, t1, 2)
+    poses, patches = D.poses.clone(), D.patches.clone()
+    fastba.BA(poses, patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj, D.kk, t0, t1,
+              M=G.M, iterations=2, plan=ws)
+    assert torch.equal(poses, P0) and torch.equal(patches, K0)
+    assert cb.check_status(poses) == 0
+
+
+def test_reproject_plan_fused_unsupported_window_raises(gpu):
+    """Outside the window path (E > 4096) the fused launch reports
+    unsupported (as fastba.plan returns None there) and writes nothing."""
+    from dpvo_amd import fastba
+
+    G = synthetic.make_dpvo_window(M=18, seed=18)  # E = 7092
+    D = G.to(gpu)
+    assert not fastba.cuda_ba.plan_supported(int(D.ii.numel()), G.F - 10, G.F, 3)
+    with pytest.raises(RuntimeError, match="unsupported"):
+        fastba.reproject(D.poses, D.patches, D.intrinsics, D.ii, D.jj, D.kk, mem=G.F,
+                         plan_window=(G.F - 10, G.F))
+
+
 def test_bad_patch_index_raises(cb, gpu):
     G = synthetic.make_config("cfg1", seed=3)
     G.kk = G.kk.clone()

@@ -60,6 +60,9 @@ def test_ba_matches_reference_ba_py(gpu, name):
     cb.forward(poses, patches, _t(z["intrinsics"], gpu), _t(z["target"], gpu), _t(z["weight"], gpu),
                torch.tensor([float(z["lmbda"])], device=gpu), _t(z["ii"], gpu), _t(z["jj"], gpu),
                _t(z["kk"], gpu), M, t0, t1, 1, False)
+    # a non-zero BA status (e.g. a spin-wait timeout, bit 16) raises here with
+    # its cause, instead of surfacing only as a numeric mismatch below
+    cb.check_status(poses)
     P, K = poses.cpu().numpy(), patches.cpu().numpy()
     # tight against the reference's fp64 run (our reductions/solve are fp64)
     np.testing.assert_allclose(P, z["out_poses64"], rtol=0, atol=1e-5)
