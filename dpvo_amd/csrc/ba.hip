@@ -1054,6 +1054,7 @@ int ba_window_launch(float* poses, float* patches, const float* intrinsics, cons
                      int iterations, char* scratch, int* status, int64_t* marks, void* stream);
 int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
                    int num_poses, int t0, int t1, char* scratch, int* status, void* stream);
+void ba_window_plan_offsets(int E, int64_t* out);
 int ba_window_reproject_plan(const float* poses, const float* patches, const float* intrinsics,
                              const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int P,
                              int num_poses, int num_patches, int N2, float* coords, int* order,
@@ -1334,6 +1335,15 @@ DPVO_EXPORT int dpvo_ba_forward(float* poses, float* patches, const float* intri
 
 DPVO_EXPORT int dpvo_ba_plan_supported(int E, int t0, int t1, int P) {
   return (g_ba_path == 0 || g_ba_path == 5) && ba_window_supported(E, t1 - t0, P) ? 1 : 0;
+}
+
+DPVO_EXPORT int dpvo_ba_plan_offsets(int E, int t0, int t1, int64_t* out) {
+  if (E <= 0 || t1 < t0 || !out) return DPVO_ERR_INVALID;
+  if (!ba_window_supported(E, t1 - t0, 3)) return DPVO_ERR_UNSUPPORTED;
+  const int64_t base = (int64_t)ba_layout(E, t1 - t0, nullptr, nullptr);
+  ba_window_plan_offsets(E, out);
+  for (int k = 0; k < 5; k++) out[k] += base;
+  return DPVO_OK;
 }
 
 DPVO_EXPORT int dpvo_ba_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E,

@@ -51,6 +51,7 @@ constexpr unsigned kFix = 0xFF;         // pose code: fixed pose
 constexpr unsigned kHbm = 0xFE;         // pose slot: read from HBM
 constexpr int kChunk = 256;             // relevant edges per pass-1 chunk
 constexpr int kPart = 42;               // doubles per published partial block
+constexpr int kPartPad = 48;            // slot stride: 384 B = 3 whole 128-B lines per slot
 constexpr long long kSpin = 2000000;    // 20 ms of the 100 MHz wall clock
 constexpr int kEpochWord = kWMaxG;      // flags[kWMaxG]: epoch of the last call
 constexpr int kFlagWords = kWMaxG + 8;
@@ -81,7 +82,7 @@ struct WArgs {
   const int64_t* kk;
   int E, P, num_poses, num_patches, t0, N, iters, NB, Sd, So, G;
   Plan plan;
-  double* part;      // [G][kPart] published partial blocks
+  double* part;      // [2][G][kPartPad] published partial blocks, by iteration parity
   long long* flags;  // persistent [kFlagWords]
   float* ejg;        // [G][E][12] per relevant edge E entries (fp32), HBM fallback
   int* status;       // [1] OR of status bits (workspace meta)
@@ -208,6 +209,10 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
       const int a = hist[v], b = (v + 1 < R) ? hist[v + 1] : E;
       if (b > a) head[a] = 1;
     }
+    // every bucket start must be read before any wave bumps it below (without
+    // this barrier a fast wave's scatter moved a slow wave's head flag into the
+    // middle of a bucket: patches split or merged, a wrong Schur complement)
+    __syncthreads();
     for (int e = tid; e < E; e += T) spos[atomicAdd(&hist[key_of(e)], 1)] = e;
     __syncthreads();
     // deterministic order inside a patch (ascending edge index): every edge
@@ -555,6 +560,9 @@ __device__ void reduce_acc(const double* acc, double* red, double* out) {
     const double v = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
     __hip_atomic_store(out + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // the storing wave drains its stores before the workgroup barrier that
+  // precedes the flag (MI355X_MICROARCH.md "Valid forms": producer)
+  if (tid < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
@@ -567,7 +575,11 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   const float fx = A.intrinsics[0], fy = A.intrinsics[1], cx = A.intrinsics[2],
               cy = A.intrinsics[3];
   // this call's tag: every workgroup reads it at entry; workgroup 0 advances it
-  // at its very end (after everyone has read it: they all arrive in iteration 0)
+  // at its very end, after everyone has read it: each workgroup's read is
+  // program-ordered before its RELEASED iteration-0 flag, which workgroup 0
+  // acquires before the advance.  Across calls the kernel boundary orders the
+  // advance before the next call's reads (a relaxed agent-scope load reads
+  // the coherent value), so neither side needs its own fence.
   const long long epoch =
       __hip_atomic_load(&A.flags[kEpochWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   mark(A, 0);
@@ -632,7 +644,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   const size_t solve_b =
       sizeof(double) * (36 * (NN * (NN + 1) / 2) + 6 * NN) + wsolve_bytes((int)NN) + 64;
   // gather: S, y and a copy of every published partial (read with one wave of loads)
-  const size_t gather_b = sizeof(double) * (36 * (NN * (NN + 1) / 2) + 6 * NN + (size_t)kPart * A.G);
+  const size_t gather_b = sizeof(double) * (36 * (NN * (NN + 1) / 2) + 6 * NN + (size_t)kPartPad * A.G);
   size_t region_b = chunk_b > red_b ? chunk_b : red_b;
   region_b = region_b > solve_b ? region_b : solve_b;
   region_b = region_b > gather_b ? region_b : gather_b;
@@ -824,7 +836,11 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     }
     // ---- linearise + assemble this workgroup's block ----
     double acc[36];
-    double* part = A.part + (size_t)g * kPart;
+    // partials double-buffered by iteration parity: a workgroup can only reach
+    // buffer it & 1 again (iteration it + 2) after every workgroup has published
+    // iteration it + 1, i.e. after each finished reading iteration it's slots
+    double* const pbuf = A.part + (size_t)(it & 1) * A.G * kPartPad;
+    double* part = pbuf + (size_t)g * kPartPad;
     double* red = reinterpret_cast<double*>(L.region);
     if (NB == 0) {
       assemble<0>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, acc);
@@ -839,7 +855,10 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     if (NB == 0) continue;  // structure only: dZ = Q u, applied after the loop
     __syncthreads();
     if (tid == 0) {
+      // release, then an explicit wait: the compiler may drop the one after
+      // buffer_wbl2 (MI355X_MICROARCH.md "Compiler hazard")
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(&A.flags[g], epoch * 64 + it + 1, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -848,29 +867,34 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       bool ok = true;
       for (int w = tid; w < A.G; w += 64) ok = wait_flag(&A.flags[w], epoch * 64 + it + 1) && ok;
       if (!ok) ctl[cTimeout] = 1;
-      // no acquire fence (it would invalidate this XCD's L2 under every one of
-      // the G workgroups): the partials are read below with agent-scope atomic
-      // loads, which go to the coherence point, issued after the flags were seen
+      // consumer: relaxed poll -> ONE agent acquire (this CU's L1) -> wait ->
+      // workgroup barrier -> plain loads of the partials
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     mark(A, mb + 1);
     const int NNb = N;
     double* Sd = reinterpret_cast<double*>(L.region);
     double* yd = Sd + 36 * NB;
-    double* pc = yd + 6 * N;  // [G][kPart] copy of the partials
+    double* pc = yd + 6 * N;  // [G][kPartPad] copy of the partials
     {
-      const int tot_p = kPart * A.G;
-      constexpr int kIn = 24;  // loads in flight per thread: one round for G <= 146 (cfg2: 99)
+      // 16-B plain loads (after the acquire above), kIn in flight per thread:
+      // one round for G <= 256
+      const int tot_p = kPartPad / 2 * A.G;
+      const double2* src = reinterpret_cast<const double2*>(pbuf);
+      double2* dst = reinterpret_cast<double2*>(pc);
+      constexpr int kIn = 24;
       for (int t0_ = tid; t0_ < tot_p; t0_ += kIn * kWT) {
-        double v[kIn];
+        double2 v[kIn];
 #pragma unroll
         for (int r = 0; r < kIn; r++) {
           const int t = t0_ + r * kWT;
-          v[r] = (t < tot_p) ? __hip_atomic_load(A.part + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+          v[r] = (t < tot_p) ? src[t] : make_double2(0.0, 0.0);
         }
 #pragma unroll
         for (int r = 0; r < kIn; r++)
-          if (t0_ + r * kWT < tot_p) pc[t0_ + r * kWT] = v[r];
+          if (t0_ + r * kWT < tot_p) dst[t0_ + r * kWT] = v[r];
       }
     }
     __syncthreads();
@@ -882,19 +906,19 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
         const int x = k / 6, z = k % 6;
         const int xx = x >= z ? x : z, zz = x >= z ? z : x;
         const int li = xx * (xx + 1) / 2 + zz;
-        for (int sb = 0; sb < A.Sd; sb++) s += pc[(ba_ * A.Sd + sb) * kPart + li];
+        for (int sb = 0; sb < A.Sd; sb++) s += pc[(ba_ * A.Sd + sb) * kPartPad + li];
         if (x == z) s += 1e-4 * s + 1.0;  // S += I (1e-4 S + 1) (ba_cuda.cu:560)
       } else {
         const int o = ba_ * (ba_ - 1) / 2 + bb_;
         const int g0 = NNb * A.Sd + o * A.So;
-        for (int sb = 0; sb < A.So; sb++) s += pc[(g0 + sb) * kPart + k];
+        for (int sb = 0; sb < A.So; sb++) s += pc[(g0 + sb) * kPartPad + k];
       }
       Sd[t] = s;
     }
     for (int t = tid; t < 6 * N; t += kWT) {
       const int i = t / 6, x = t % 6;
       double s = 0.0;
-      for (int sb = 0; sb < A.Sd; sb++) s += pc[(i * A.Sd + sb) * kPart + 21 + x];
+      for (int sb = 0; sb < A.Sd; sb++) s += pc[(i * A.Sd + sb) * kPartPad + 21 + x];
       yd[t] = s;
     }
     __syncthreads();
@@ -1015,16 +1039,41 @@ static WGrid window_grid(int E, int N) {
   return w;
 }
 
+// Workgroups of ba_window_kernel the current device can hold at once (its
+// grid exchange needs every workgroup resident): CUs x blocks per CU, asked
+// once per device.  0 if the runtime cannot say (then nothing is supported).
+static int window_coresident() {
+  static std::mutex mu;
+  static std::map<int, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int cus = 0, per = 0;
+  (void)hipFuncSetAttribute((const void*)ba_window_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)ba_window_kernel, kWT,
+                                                   kWLds) != hipSuccess) {
+    (void)hipGetLastError();
+    cus = per = 0;
+  }
+  cache[dev] = cus * per;
+  return cus * per;
+}
+
 bool ba_window_supported(int E, int N, int P) {
   if (E <= 0 || E > kWMaxE || N < 0 || N > kWMaxN || P < 2 || P * P > 64) return false;
-  return window_grid(E, N).G <= kWMaxG;
+  const int G = window_grid(E, N).G;
+  return G <= kWMaxG && G <= window_coresident();
 }
 
 size_t ba_window_scratch_bytes(int E, int N) {
   const WGrid w = window_grid(E, N);
   return al256w(sizeof(int) * (size_t)E) + al256w(sizeof(int) * (size_t)(E + 1)) +
          al256w(sizeof(unsigned) * (size_t)E) + al256w(sizeof(int) * (size_t)E) +
-         al256w(sizeof(int) * 8) + al256w(sizeof(double) * kPart * (size_t)w.G) +
+         al256w(sizeof(int) * 8) + al256w(sizeof(double) * 2 * kPartPad * (size_t)w.G) +
          al256w(sizeof(float) * 16 * (size_t)w.G * E);
 }
 
@@ -1062,6 +1111,15 @@ void ba_set_status_sink(int* sink) {
   (void)hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_sink_mu);
   g_sink[dev] = sink;
+}
+
+// byte offsets of the plan arrays inside the window scratch (tests, tools)
+void ba_window_plan_offsets(int E, int64_t* out) {
+  out[0] = 0;                                                  // epos [E]
+  out[1] = out[0] + (int64_t)al256w(sizeof(int) * (size_t)E);  // poff [E + 1]
+  out[2] = out[1] + (int64_t)al256w(sizeof(int) * (size_t)(E + 1));  // pmask [E]
+  out[3] = out[2] + (int64_t)al256w(sizeof(unsigned) * (size_t)E);  // pkk [E]
+  out[4] = out[3] + (int64_t)al256w(sizeof(int) * (size_t)E);  // meta [8]: nuniq, fmin, status
 }
 
 static Plan plan_view(char* scratch, int E, int* status) {
@@ -1168,7 +1226,7 @@ int ba_window_run(float* poses, float* patches, const float* intrinsics, const f
             al256w(sizeof(unsigned) * (size_t)E) + al256w(sizeof(int) * (size_t)E) +
             al256w(sizeof(int) * 8);
   a.part = (double*)s;
-  s += al256w(sizeof(double) * kPart * (size_t)w.G);
+  s += al256w(sizeof(double) * 2 * kPartPad * (size_t)w.G);
   a.ejg = (float*)s;
   a.poses = poses;
   a.patches = patches;

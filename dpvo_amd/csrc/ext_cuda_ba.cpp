@@ -212,6 +212,12 @@ torch::Tensor ba_plan(torch::Tensor ii, torch::Tensor jj, torch::Tensor kk, int6
   return ws;
 }
 
+std::vector<int64_t> ba_plan_offsets(int64_t E, int t0, int t1) {
+  std::vector<int64_t> o(5);
+  check_status(dpvo_ba_plan_offsets((int)E, t0, t1, o.data()), "cuda_ba.plan_offsets");
+  return o;
+}
+
 void ba_forward_planned(torch::Tensor ws, torch::Tensor poses, torch::Tensor patches,
                         torch::Tensor intrinsics, torch::Tensor target, torch::Tensor weight,
                         torch::Tensor lmbda, torch::Tensor ii, torch::Tensor jj, torch::Tensor kk,
@@ -661,6 +667,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pg_remove", &pg_remove, "PatchGraph.remove_factors on the device (dpvo.py:523-568)");
   m.def("plan_supported", &ba_plan_supported, "window path available for (E, t0, t1, P)");
   m.def("plan", &ba_plan, "group the edges by patch (reads ii/jj/kk only) -> workspace");
+  m.def("plan_offsets", &ba_plan_offsets,
+        "byte offsets of epos, poff, pmask, pkk, meta inside a plan workspace");
   m.def("forward_planned", &ba_forward_planned, "BA iterations on a planned workspace");
   m.def("check_status", &ba_check_status,
         "sync on the BA status of every forward so far on the device of `like`; raises "

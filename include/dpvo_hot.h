@@ -225,6 +225,13 @@ int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1, int* out, 
    dpvo_ba_plan_supported() accepts (the window path: E <= 4096, N <= 16,
    P * P <= 64); otherwise call dpvo_ba_forward. */
 int dpvo_ba_plan_supported(int E, int t0, int t1, int P);
+/* Byte offsets, inside a dpvo_ba_plan workspace, of the plan arrays:
+   out[0] epos int32[E] (edge at sorted position p, grouped by patch, ascending
+   edge index inside a patch), out[1] poff int32[E+1] (first position of patch
+   u), out[2] pmask uint32[E] (free-pose bits of patch u), out[3] pkk int32[E]
+   (kk of patch u, ascending), out[4] meta int32[8] (nuniq, fixed-pose minimum,
+   status).  For tests and tools; no reference counterpart. */
+int dpvo_ba_plan_offsets(int E, int t0, int t1, int64_t* out);
 int dpvo_ba_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
                  int num_poses, int t0, int t1, void* workspace, size_t workspace_bytes,
                  void* stream);

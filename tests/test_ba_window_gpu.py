@@ -168,3 +168,74 @@ def test_large_graph_structure_limit_raises(cb, gpu):
     _run(cb, G, gpu, 1, G.F, 1)
     with pytest.raises(RuntimeError, match="status"):
         cb.check_status(G.poses.to(gpu))
+
+
+def _host_grouping(ii, jj, kk, t0, t1):
+    """numpy restatement of the plan: patches in ascending kk, edges of a
+    patch in ascending edge index, free-pose bits of t0 <= ii/jj < t1."""
+    order = np.lexsort((np.arange(kk.size), kk))
+    uk, first = np.unique(kk[order], return_index=True)
+    poff = np.append(first, kk.size)
+    N = t1 - t0
+    bits = np.zeros(kk.size, np.uint32)
+    for x in (ii, jj):
+        free = (x >= t0) & (x < t1)
+        bits |= np.where(free, np.left_shift(1, np.clip(x - t0, 0, 31)), 0).astype(np.uint32)
+    pmask = np.array([np.bitwise_or.reduce(bits[order[poff[u]:poff[u + 1]]])
+                      for u in range(uk.size)], np.uint32)
+    assert N <= 16
+    return order.astype(np.int32), poff.astype(np.int32), pmask, uk.astype(np.int32)
+
+
+def _plan_arrays(cb, ws, E, t0, t1):
+    off = cb.plan_offsets(E, t0, t1)
+    b = ws.cpu().numpy()
+
+    def arr(k, n, dt):
+        return np.frombuffer(b[off[k]:off[k] + 4 * n].tobytes(), dt)
+
+    nuniq = int(arr(4, 8, np.int32)[0])
+    return (arr(0, E, np.int32), arr(1, nuniq + 1, np.int32), arr(2, nuniq, np.uint32),
+            arr(3, nuniq, np.int32), nuniq)
+
+
+@pytest.mark.parametrize("E,nk,M,seed", [(96, 40, 1024, 0), (700, 650, 1024, 1),
+                                         (3000, 2500, 1024, 2), (4096, 300, 1024, 3),
+                                         (4000, 3900, 1024, 4), (2048, 1500, 2048, 5)])
+def test_plan_grouping_matches_host(cb, gpu, E, nk, M, seed):
+    """Regression for the plan's counting sort (the head flags of every
+    bucket are read before any wave bumps a bucket counter): many small
+    buckets and E > 64, through fastba.plan and the fused reprojection launch,
+    the grouping is exactly the host one, on repeated calls.  M = 2048 puts
+    the kk range past the counting sort's (bitonic path)."""
+    from dpvo_amd import fastba
+
+    rng = np.random.default_rng(seed)
+    F = 12
+    t0, t1 = 1, F
+    base = np.sort(rng.choice(F * M, nk, replace=False))
+    kk = np.concatenate([base, base[rng.integers(0, nk, E - nk)]])
+    kk = rng.permutation(kk).astype(np.int64)
+    ii = kk // M
+    jj = rng.integers(0, F, E).astype(np.int64)
+    ref = _host_grouping(ii, jj, kk, t0, t1)
+    D = [torch.from_numpy(x).to(gpu) for x in (ii, jj, kk)]
+    for rep in range(3):
+        ws = fastba.plan(*D, t0, t1, F * M, F)
+        assert ws is not None
+        epos, poff, pmask, pkk, nuniq = _plan_arrays(cb, ws, E, t0, t1)
+        assert nuniq == ref[3].size
+        np.testing.assert_array_equal(pkk, ref[3])
+        np.testing.assert_array_equal(poff, ref[1])
+        np.testing.assert_array_equal(epos, ref[0])
+        np.testing.assert_array_equal(pmask, ref[2])
+    # the same grouping from workgroup 0 of the fused reprojection launch
+    poses = torch.zeros(F, 7, device=gpu)
+    poses[:, 6] = 1
+    patches = torch.ones(F * M, 3, 3, 3, device=gpu)
+    intr = torch.tensor([[80.0, 80.0, 80.0, 60.0]], device=gpu).repeat(F, 1)
+    _, _, ws = fastba.reproject(poses, patches, intr, *D, mem=F, plan_window=(t0, t1))
+    epos, poff, pmask, pkk, _ = _plan_arrays(cb, ws, E, t0, t1)
+    np.testing.assert_array_equal(epos, ref[0])
+    np.testing.assert_array_equal(pkk, ref[3])
+    np.testing.assert_array_equal(pmask, ref[2])
