@@ -1,0 +1,181 @@
+// Standalone check + timing of the window solvers: ba_ldl.hpp ldl_solve (new)
+// against ba_solve.hpp wsolve (round 2), one 256-thread workgroup, random SPD
+// systems shaped like a DPVO window (Gram matrix + the reference's damping),
+// against a host fp64 Cholesky.  Prints rel. error and shader cycles.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I dpvo_amd/csrc -I scripts/micro \
+//         scripts/micro/ldl_bench.hip -o scripts/micro/ldl_bench
+//   ./scripts/micro/ldl_bench [N=11] [refine=1] [cond_scale=300]
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "ba_ldl_experiment.hpp"
+#include "ba_solve.hpp"
+
+using namespace dpvo::bad;
+
+template <int KIND, int DBG = 0>
+__global__ void __launch_bounds__(256) k_solve(const double* S, const double* y, int N, int refine,
+                                               double* dX, long long* cyc, int* fail, long long* stg) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int NB = N * (N + 1) / 2, n = 6 * N;
+  double* Sd = (double*)lds;
+  double* yd = Sd + 36 * NB;
+  __shared__ int f;
+  __shared__ long long stl[64];
+  for (int k = threadIdx.x; k < 36 * NB; k += blockDim.x) Sd[k] = S[k];
+  for (int k = threadIdx.x; k < n; k += blockDim.x) yd[k] = y[k];
+  __syncthreads();
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  bool ok;
+  double* xo;
+  if (KIND == 0) {
+    WSolve s;
+    s.S = Sd;
+    s.y = yd;
+    s.x = yd + n;
+    s.r = s.x + n;
+    s.A = (float*)(s.r + n);
+    s.Z = s.A + 36 * NB;
+    s.v0 = s.Z + 36 * NB;
+    s.v1 = s.v0 + n;
+    ok = wsolve(s, N, refine, &f);
+    xo = s.x;
+  } else {
+    LSolve v = ldl_view(Sd, yd, (char*)(yd + n), N, &f);
+    ok = ldl_solve(v, N, refine, stl, DBG);
+    xo = v.x;
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  for (int k = threadIdx.x; k < n; k += blockDim.x) dX[k] = xo[k];
+  for (int k = threadIdx.x; k < 64; k += blockDim.x) stg[k] = stl[k];
+  if (threadIdx.x == 0) {
+    *cyc = t1 - t0;
+    *fail = ok ? 0 : 1;
+  }
+}
+
+static int lb(int a, int b) { return a * (a + 1) / 2 + b; }
+
+template <int KIND, int DBG = 0>
+static void run(const char* name, int N, int refine, double* dS, double* dy, double* dX,
+                long long* dc, int* dfail, long long* dst, const std::vector<double>& ref) {
+  const int n = 6 * N, NB = N * (N + 1) / 2;
+  const size_t lds = 150 * 1024;
+  hipFuncSetAttribute((const void*)(k_solve<KIND, DBG>), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  std::vector<long long> cs;
+  for (int r = 0; r < 40; r++) {
+    hipLaunchKernelGGL((k_solve<KIND, DBG>), dim3(1), dim3(256), lds, 0, dS, dy, N, refine, dX, dc, dfail, dst);
+    hipDeviceSynchronize();
+    long long c;
+    hipMemcpy(&c, dc, sizeof(c), hipMemcpyDeviceToHost);
+    cs.push_back(c);
+  }
+  std::sort(cs.begin(), cs.end());
+  std::vector<double> got(n);
+  int fail = 0;
+  hipMemcpy(got.data(), dX, sizeof(double) * n, hipMemcpyDeviceToHost);
+  hipMemcpy(&fail, dfail, sizeof(int), hipMemcpyDeviceToHost);
+  double e = 0, nr = 0;
+  for (int i = 0; i < n; i++) {
+    e += (got[i] - ref[i]) * (got[i] - ref[i]);
+    nr += ref[i] * ref[i];
+  }
+  if (KIND == 1) {
+    long long h[64];
+    hipMemcpy(h, dst, sizeof(h), hipMemcpyDeviceToHost);
+    printf("   copy %lld panel0 %lld steps", h[1] - h[0], h[2] - h[1]);
+    for (int k = 0; k < N; k++) printf(" %lld", h[3 + k] - h[2 + k]);
+    printf(" | prep %lld back %lld", h[39] - h[2 + N], h[40] - h[39]);
+    printf(" | trl k7: pre %lld ld %lld mfma %lld st %lld (from step start %lld)", h[51] - h[50], h[52] - h[51], h[53] - h[52], 0LL, h[50] - h[2 + 7]);
+    for (int it = 0; it < refine; it++)
+      printf(" | res %lld chains %lld", h[41 + 2 * it] - (it ? h[40 + 2 * it] : h[40]),
+             h[42 + 2 * it] - h[41 + 2 * it]);
+    printf("\n");
+  }
+  printf("%-6s N=%2d refine=%d fail=%d rel.err=%.3e median=%6lld cyc (%.2f us @2.4GHz)\n", name, N,
+         refine, fail, sqrt(e / nr), cs[cs.size() / 2], cs[cs.size() / 2] / 2400.0);
+  (void)NB;
+}
+
+int main(int argc, char** argv) {
+  const int N0 = argc > 1 ? atoi(argv[1]) : 0;
+  const int refine = argc > 2 ? atoi(argv[2]) : 1;
+  const double scale = argc > 3 ? atof(argv[3]) : 300.0;
+  double *dS, *dy, *dX;
+  long long* dc;
+  int* dfail;
+  hipMalloc(&dS, sizeof(double) * 36 * 136);
+  hipMalloc(&dy, sizeof(double) * 96);
+  hipMalloc(&dX, sizeof(double) * 96);
+  hipMalloc(&dc, sizeof(long long));
+  hipMalloc(&dfail, sizeof(int));
+  long long* dst;
+  hipMalloc(&dst, sizeof(long long) * 64);
+  hipMemset(dst, 0, sizeof(long long) * 64);
+  const int Ns[] = {1, 2, 5, 10, 11, 12, 16};
+  for (int N : Ns) {
+    if (N0 && N != N0) continue;
+    const int n = 6 * N, NB = N * (N + 1) / 2;
+    srand(1 + N);
+    std::vector<double> G(n * 2 * n), D(n * n, 0.0), y(n);
+    for (auto& v : G) v = (rand() / (double)RAND_MAX - 0.5) * scale;
+    for (int i = 0; i < n; i++)
+      for (int j = 0; j < n; j++) {
+        double s = 0;
+        for (int k = 0; k < 2 * n; k++)
+          s += G[i * 2 * n + k] * G[j * 2 * n + k] * (k % 7 == 0 ? 1e-3 : 1.0);
+        D[i * n + j] = s;
+      }
+    for (int i = 0; i < n; i++) D[i * n + i] += 1e-4 * D[i * n + i] + 1.0;
+    for (auto& v : y) v = rand() / (double)RAND_MAX - 0.5;
+    std::vector<double> Sb(36 * NB);
+    for (int a = 0; a < N; a++)
+      for (int b = 0; b <= a; b++)
+        for (int x = 0; x < 6; x++)
+          for (int z = 0; z < 6; z++) Sb[36 * lb(a, b) + 6 * x + z] = D[(6 * a + x) * n + 6 * b + z];
+    std::vector<double> L(n * n, 0.0), ref(n), z(n);
+    for (int j = 0; j < n; j++) {
+      double s = D[j * n + j];
+      for (int k = 0; k < j; k++) s -= L[j * n + k] * L[j * n + k];
+      L[j * n + j] = sqrt(s);
+      for (int i = j + 1; i < n; i++) {
+        double t = D[i * n + j];
+        for (int k = 0; k < j; k++) t -= L[i * n + k] * L[j * n + k];
+        L[i * n + j] = t / L[j * n + j];
+      }
+    }
+    for (int i = 0; i < n; i++) {
+      double s = y[i];
+      for (int k = 0; k < i; k++) s -= L[i * n + k] * z[k];
+      z[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+      double s = z[i];
+      for (int k = i + 1; k < n; k++) s -= L[k * n + i] * ref[k];
+      ref[i] = s / L[i * n + i];
+    }
+    double dmin = 1e300, dmax = 0;
+    for (int i = 0; i < n; i++) {
+      dmin = std::min(dmin, L[i * n + i]);
+      dmax = std::max(dmax, L[i * n + i]);
+    }
+    printf("N=%d cond~%.1e\n", N, (dmax * dmax) / (dmin * dmin));
+    hipMemcpy(dS, Sb.data(), sizeof(double) * Sb.size(), hipMemcpyHostToDevice);
+    hipMemcpy(dy, y.data(), sizeof(double) * n, hipMemcpyHostToDevice);
+    if (argc > 4) {  // only the ldl solve (profiling)
+      run<1>("ldl", N, refine, dS, dy, dX, dc, dfail, dst, ref);
+      continue;
+    }
+    run<0>("wsolve", N, refine, dS, dy, dX, dc, dfail, dst, ref);
+    run<1>("ldl", N, refine, dS, dy, dX, dc, dfail, dst, ref);
+    run<1>("ldl-r0", N, 0, dS, dy, dX, dc, dfail, dst, ref);
+    run<1, 1>("no-trl", N, 1, dS, dy, dX, dc, dfail, dst, ref);
+    run<1, 2>("no-la", N, 1, dS, dy, dX, dc, dfail, dst, ref);
+  }
+  return 0;
+}
