@@ -1,5 +1,6 @@
 // ba_window.hip -- F-BA for DPVO local-BA windows (N <= 16 free poses,
-// E <= 4096 edges): the default path of cuda_ba.forward for those shapes.
+// E <= 10240 edges, DPVO MAX_EDGES = 10000): the default path of
+// cuda_ba.forward for those shapes.
 //
 // Reference semantics: dpvo/fastba/ba_cuda.cu:433-582 (block_e.cu:188-300 for
 // the block-sparse E):
@@ -42,7 +43,7 @@ using namespace bad;
 constexpr int kWT = 256;                // iteration kernel threads
 constexpr int kPT = 512;                // plan kernel threads
 constexpr int kWMaxN = 16;
-constexpr int kWMaxE = 4096;
+constexpr int kWMaxE = 10240;           // DPVO MAX_EDGES = 10000 (config.py:42)
 constexpr int kWMaxG = 256;
 constexpr int kWLds = 160 * 1024;
 constexpr int kHistMax = 12288;         // counting-sort range of kk
@@ -84,7 +85,7 @@ struct WArgs {
   Plan plan;
   double* part;      // [2][G][kPartPad] published partial blocks, by iteration parity
   long long* flags;  // persistent [kFlagWords]
-  float* ejg;        // [G][E][12] per relevant edge E entries (fp32), HBM fallback
+  float* ejg;        // [2][E][12] E entries by edge and iteration parity (fp32), HBM fallback
   int* status;       // [1] OR of status bits (workspace meta)
   int* sink;         // caller's sticky status word (dpvo_ba_set_status_sink) or null
   int64_t* marks;    // [64] wall-clock stamps of workgroup 0 (may be null)
@@ -130,12 +131,18 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
                                            const int64_t* __restrict__ kk, int E, int num_patches,
                                            int num_poses, int t0, int N, const Plan& plan,
                                            char* lds) {
+  // LDS (153.9 KB at kWMaxE = 10240): per-edge arrays as u16 / u8, one union
+  //   [ctl 256 B | code u16[E] | key u16[E] -> ranked | spos u16[E] | head u8[E] | U 80 KB]
+  //   U: counting sort hist int[kHistMax], later hd int[E] + mask u32[E];
+  //      bitonic sort keys (u64 for E <= 8192, u32 (key << 14 | e) above)
   const int tid = threadIdx.x, lane = tid & 63, T = kPT;
   int* ctl = (int*)lds;                  // [64]
   int* scr = ctl + 16;                   // scan scratch [>= 17]
-  unsigned* code = (unsigned*)(lds + 256);                        // [E] ci | cj << 8
-  int* kkv = (int*)(lds + 256 + al16(sizeof(unsigned) * kWMaxE)); // [E] kk (clamped)
-  char* big = lds + 256 + 2 * al16(sizeof(unsigned) * kWMaxE);   // sort area
+  unsigned short* code = (unsigned short*)(lds + 256);           // ci | cj << 8 (5 bits each)
+  unsigned short* key = code + kWMaxE;                           // kk - kmin, later ranked edges
+  unsigned short* spos = key + kWMaxE;                           // edge at position p
+  unsigned char* head = (unsigned char*)(spos + kWMaxE);         // head flags
+  char* U = (char*)head + al16(kWMaxE);
   const int kmaxc = num_patches - 1;
   if (tid == 0) {
     ctl[0] = 0x7fffffff;  // kmin
@@ -144,22 +151,25 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
     ctl[3] = 0;           // status
   }
   __syncthreads();
+  constexpr int kPer = kWMaxE / kPT;  // edges per thread: e = tid + r * T
+  int kv[kPer];                      // clamped kk of this thread's edges (registers)
   int kmin = 0x7fffffff, kmax = -1, fmin = 0x7fffffff, bad = 0;
-  {
-    // every load of the edge list issued before the first use: ONE global
-    // round trip (a strided loop with the uses inside waits once per pass)
-    constexpr int kPer = kWMaxE / kPT;
-    int64_t vk[kPer], vi[kPer], vj[kPer];
+  // the edge list in rounds of 8 edges per thread, every load of a round issued
+  // before its first use (one global round trip per round)
 #pragma unroll
-    for (int r = 0; r < kPer; r++) {
-      const int e = tid + r * T;
+  for (int r0 = 0; r0 < kPer; r0 += 4) {
+    int64_t vk[4], vi[4], vj[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int e = tid + (r0 + r) * T;
       vk[r] = (e < E) ? kk[e] : 0;
       vi[r] = (e < E) ? ii[e] : 0;
       vj[r] = (e < E) ? jj[e] : 0;
     }
 #pragma unroll
-    for (int r = 0; r < kPer; r++) {
-      const int e = tid + r * T;
+    for (int r = 0; r < 4; r++) {
+      const int e = tid + (r0 + r) * T;
+      kv[r0 + r] = 0;
       if (e >= E) continue;
       int64_t v = vk[r];
       if (v < 0 || v > kmaxc) {
@@ -168,13 +178,13 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
       }
       kmin = min(kmin, (int)v);
       kmax = max(kmax, (int)v);
-      kkv[e] = (int)v;
+      kv[r0 + r] = (int)v;
       const int64_t gi = vi[r], gj = vj[r];
       const bool fi = gi >= t0 && gi < t0 + N, fj = gj >= t0 && gj < t0 + N;
       const int ci = fi ? (int)(gi - t0) : (int)kFix, cj = fj ? (int)(gj - t0) : (int)kFix;
       if (!fi) fmin = min(fmin, (int)min(max(gi, (int64_t)0), (int64_t)num_poses - 1));
       if (!fj) fmin = min(fmin, (int)min(max(gj, (int64_t)0), (int64_t)num_poses - 1));
-      code[e] = (unsigned)ci | ((unsigned)cj << 8);
+      code[e] = (unsigned short)((ci & 0xff) | ((cj & 0xff) << 8));
     }
   }
 #pragma unroll
@@ -193,18 +203,19 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
   __syncthreads();
   kmin = ctl[0];
   const int R = ctl[1] - kmin + 1;
-  int* spos = (int*)big;                 // [E] edge at position p
-  int* head = spos + kWMaxE;             // [E] head flags -> patch index (scan)
-  auto key_of = [&](int e) -> int { return kkv[e] - kmin; };
+  unsigned short* pos_edge = spos;  // the sorted order, wherever it ends up
   if (R <= kHistMax) {
-    int* hist = head + kWMaxE;           // [R]
+    int* hist = (int*)U;  // [R]
     for (int v = tid; v < R; v += T) hist[v] = 0;
-    __syncthreads();
-    for (int e = tid; e < E; e += T) atomicAdd(&hist[key_of(e)], 1);
-    __syncthreads();
-    fscan(hist, R, scr);                 // hist[v] = first position of bucket v
     for (int p = tid; p < E; p += T) head[p] = 0;
     __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const int e = tid + r * T;
+      if (e < E) atomicAdd(&hist[kv[r] - kmin], 1);
+    }
+    __syncthreads();
+    fscan(hist, R, scr);  // hist[v] = first position of bucket v
     for (int v = tid; v < R; v += T) {
       const int a = hist[v], b = (v + 1 < R) ? hist[v + 1] : E;
       if (b > a) head[a] = 1;
@@ -213,27 +224,60 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
     // this barrier a fast wave's scatter moved a slow wave's head flag into the
     // middle of a bucket: patches split or merged, a wrong Schur complement)
     __syncthreads();
-    for (int e = tid; e < E; e += T) spos[atomicAdd(&hist[key_of(e)], 1)] = e;
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const int e = tid + r * T;
+      if (e < E) spos[atomicAdd(&hist[kv[r] - kmin], 1)] = (unsigned short)e;
+    }
     __syncthreads();
     // deterministic order inside a patch (ascending edge index): every edge
-    // counts the smaller edges of its bucket, all edges in parallel (was a
-    // serial insertion sort per bucket: a chain of dependent LDS accesses)
-    int* ranked = hist + kHistMax;  // [E]
-    for (int e = tid; e < E; e += T) {
-      const int v = key_of(e);
+    // counts the smaller edges of its bucket, all edges in parallel; the
+    // ranked order overwrites the keys (no longer read) after a barrier
+    int dst[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const int e = tid + r * T;
+      dst[r] = -1;
+      if (e >= E) continue;
+      const int v = kv[r] - kmin;
       const int b = hist[v], a = (v == 0) ? 0 : hist[v - 1];  // hist[v]: end of bucket v now
       int rank = 0;
-      for (int t = a; t < b; t++) rank += (spos[t] < e) ? 1 : 0;
-      ranked[a + rank] = e;
+      for (int t = a; t < b; t++) rank += ((int)spos[t] < e) ? 1 : 0;
+      dst[r] = a + rank;
     }
-    spos = ranked;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kPer; r++)
+      if (dst[r] >= 0) key[dst[r]] = (unsigned short)(tid + r * T);
+    pos_edge = key;
   } else {
-    // wide kk range: bitonic sort of (key << 32 | e) over the next power of two
+    // wide kk range: bitonic sort over the next power of two of (key, e):
+    // u64 (key << 32 | e) up to E = 8192, else u32 (key << 14 | e), which
+    // needs R <= 2^18 (status 32 otherwise: the call raises)
     int P2 = 1;
     while (P2 < E) P2 <<= 1;
-    unsigned long long* keys = (unsigned long long*)(head + kWMaxE);
-    for (int i = tid; i < P2; i += T)
-      keys[i] = (i < E) ? (((unsigned long long)(unsigned)key_of(i) << 32) | (unsigned)i) : ~0ull;
+    const bool wide = P2 <= 8192;
+    if (!wide && R > (1 << 18)) {
+      if (tid == 0) ctl[3] |= kStCap;
+    }
+    unsigned long long* k64 = (unsigned long long*)U;
+    unsigned* k32 = (unsigned*)U;
+#pragma unroll
+    for (int r = 0; r < kPer; r++) {
+      const int e = tid + r * T;
+      if (e < E) {
+        if (wide)
+          k64[e] = ((unsigned long long)(unsigned)(kv[r] - kmin) << 32) | (unsigned)e;
+        else
+          k32[e] = ((unsigned)min(kv[r] - kmin, (1 << 18) - 1) << 14) | (unsigned)e;
+      }
+    }
+    for (int i = E + tid; i < P2; i += T) {
+      if (wide)
+        k64[i] = ~0ull;
+      else
+        k32[i] = ~0u;
+    }
     __syncthreads();
     for (int size = 2; size <= P2; size <<= 1)
       for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -241,44 +285,58 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
           const int lo = 2 * i - (i & (stride - 1));
           const int hi = lo + stride;
           const bool up = ((lo & size) == 0);
-          const unsigned long long a = keys[lo], b = keys[hi];
-          if ((a > b) == up) {
-            keys[lo] = b;
-            keys[hi] = a;
+          if (wide) {
+            const unsigned long long a = k64[lo], b = k64[hi];
+            if ((a > b) == up) {
+              k64[lo] = b;
+              k64[hi] = a;
+            }
+          } else {
+            const unsigned a = k32[lo], b = k32[hi];
+            if ((a > b) == up) {
+              k32[lo] = b;
+              k32[hi] = a;
+            }
           }
         }
         __syncthreads();
       }
     for (int p = tid; p < E; p += T) {
-      spos[p] = (int)(keys[p] & 0xffffffffull);
-      head[p] = (p == 0 || (keys[p] >> 32) != (keys[p - 1] >> 32)) ? 1 : 0;
+      if (wide) {
+        spos[p] = (unsigned short)(k64[p] & 0xffffffffull);
+        head[p] = (p == 0 || (k64[p] >> 32) != (k64[p - 1] >> 32)) ? 1 : 0;
+      } else {
+        spos[p] = (unsigned short)(k32[p] & 0x3fffu);
+        head[p] = (p == 0 || (k32[p] >> 14) != (k32[p - 1] >> 14)) ? 1 : 0;
+      }
     }
   }
   __syncthreads();
-  // patch index of every position: inclusive scan of the heads
-  int* hd = head;
+  // patch index of every position: exclusive scan of the heads (U is free now)
+  int* hd = (int*)U;
+  for (int p = tid; p < E; p += T) hd[p] = head[p];
+  __syncthreads();
   const int nuniq = fscan(hd, E, scr);   // hd[p] = heads strictly before p
   // patch u starts at the p with hd[p] == u and a head: recompute heads
   for (int p = tid; p < E; p += T) {
     const int u1 = (p + 1 < E) ? hd[p + 1] : nuniq;  // heads up to and including p
     const bool is_head = u1 != hd[p];
     const int u = u1 - 1;                            // patch of position p
-    const int e = spos[p];
+    const int e = pos_edge[p];
     plan.epos[p] = e;
     if (is_head) {
       plan.poff[u] = p;
-      plan.pkk[u] = key_of(e) + kmin;
+      plan.pkk[u] = (int)min(max(kk[e], (int64_t)0), (int64_t)kmaxc);
     }
   }
   if (tid == 0) plan.poff[nuniq] = E;
   // free-pose masks: OR over the patch's edges (positions are contiguous)
-  unsigned* mask = (unsigned*)(hd + kWMaxE);  // [nuniq] (past the sort keys' first half)
-  __syncthreads();
+  unsigned* mask = (unsigned*)(U + sizeof(int) * kWMaxE);  // [nuniq]
   for (int u = tid; u < nuniq; u += T) mask[u] = 0u;
   __syncthreads();
   for (int p = tid; p < E; p += T) {
     const int u = ((p + 1 < E) ? hd[p + 1] : nuniq) - 1;
-    const unsigned c = code[spos[p]];
+    const unsigned c = code[pos_edge[p]];
     const unsigned ci = c & 0xff, cj = c >> 8;
     const unsigned m = (ci != kFix ? 1u << ci : 0u) | (cj != kFix ? 1u << cj : 0u);
     if (m) atomicOr(&mask[u], m);
@@ -356,9 +414,18 @@ struct WL {  // LDS layout of one workgroup
   unsigned short* ec;  // [nrp] pose slot of ii | slot of jj << 8
   unsigned short* rp;  // [nrp] relevant patch of the edge
   int* eid;            // [nrp] edge index
-  float4* tw;          // [nrp] target, weight (LDS or HBM)
-  float* ej;           // [nrp][12] E entries of the last linearisation (LDS or HBM)
+  float4* tw;          // [nrp] target, weight (LDS), or null: read by edge from the inputs
+  float* ej;           // [nrp][12] E entries of the last linearisation (LDS), or null
   char* region;        // union: chunk scratch / reduction table / solver
+  // E entries of relevant edge q for iteration parity par: in LDS by q, else in
+  // the shared HBM buffer by edge id and parity.  Every workgroup holding an
+  // edge writes the same bits there (identical poses, depths and order), and
+  // parity keeps a workgroup one iteration ahead off the slot a slower one
+  // still reads (it can reach iteration it + 2 only after every workgroup
+  // has published it + 1, i.e. finished reading iteration it's entries)
+  __device__ __forceinline__ float* ej_at(const float* ejg, int E, int q, int par) const {
+    return ej ? ej + 12 * (size_t)q : const_cast<float*>(ejg) + ((size_t)par * E + eid[q]) * 12;
+  }
 };
 
 enum { cNrel = 0, cNrp = 1, cFmin = 2, cFail = 3, cTimeout = 4, cCap = 5, cFailAny = 6, cScan = 16 };
@@ -384,7 +451,7 @@ __device__ __forceinline__ void pose_of(const WArgs& A, const WL& L, unsigned sl
 
 template <int MODE>  // 0: only Q, u (no free pose / N == 0); 1 diagonal block; 2 off-diagonal
 __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, double lam,
-                         float fx, float fy, float cx, float cy, double* acc) {
+                         float fx, float fy, float cx, float cy, int par, double* acc) {
   constexpr int NA = (MODE == 1) ? 27 : (MODE == 2 ? 36 : 1);
   const int tid = threadIdx.x, N = A.N;
   const unsigned ua = (unsigned)a, ub = (unsigned)b;
@@ -413,7 +480,14 @@ __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, do
       pose_of(A, L, si, si == kHbm ? (int)A.ii[e] : 0, Pi);
       pose_of(A, L, sj, sj == kHbm ? (int)A.jj[e] : 0, Pj);
       const int ri = L.rp[q];
-      const float4 tw = L.tw[q];
+      float4 tw;
+      if (L.tw) {
+        tw = L.tw[q];
+      } else {
+        const float2 tg = reinterpret_cast<const float2*>(A.target)[e];
+        const float2 wt = reinterpret_cast<const float2*>(A.weight)[e];
+        tw = make_float4(tg.x, tg.y, wt.x, wt.y);
+      }
       Lin o;
       lin_edge(Pi, Pj, L.nxy[ri].x, L.nxy[ri].y, L.dep[ri], tw.x, tw.y, tw.z, tw.w, fx, fy, cx,
                cy, o);
@@ -432,7 +506,7 @@ __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, do
         uq += (wr * (double)o.r[row]) * (double)o.Jz[row];
       }
       // E entries (fp32) for the depth update after the solve
-      float4* eo = reinterpret_cast<float4*>(L.ej + 12 * (size_t)q);
+      float4* eo = reinterpret_cast<float4*>(L.ej_at(A.ejg, A.E, q, par));
       eo[0] = make_float4((float)ejv[0], (float)ejv[1], (float)ejv[2], (float)ejv[3]);
       eo[1] = make_float4((float)ejv[4], (float)ejv[5], (float)eiv[0], (float)eiv[1]);
       eo[2] = make_float4((float)eiv[2], (float)eiv[3], (float)eiv[4], (float)eiv[5]);
@@ -676,19 +750,16 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   L.rp = (unsigned short*)take(sizeof(unsigned short) * (nrp + 1));
   L.eid = (int*)take(sizeof(int) * (nrp + 1));
   L.region = take(region_b);
-  // target/weight and E entries in LDS when they fit, else this workgroup's HBM scratch
+  // target/weight and E entries in LDS when they fit; else E entries in the
+  // shared HBM buffer (WL::ej_at) and target/weight read from the inputs
   const size_t tw_b = sizeof(float4) * (nrp + 1), ej_b = sizeof(float) * 12 * (nrp + 1);
-  float4* tw_hbm = reinterpret_cast<float4*>(A.ejg + (size_t)g * A.E * 16);
-  float* ej_hbm = A.ejg + (size_t)g * A.E * 16 + 4 * (size_t)A.E;
+  L.tw = nullptr;
+  L.ej = nullptr;
   if (o2 + tw_b + ej_b <= (size_t)kWLds) {
     L.tw = (float4*)take(tw_b);
     L.ej = (float*)take(ej_b);
   } else if (o2 + tw_b <= (size_t)kWLds) {
     L.tw = (float4*)take(tw_b);
-    L.ej = ej_hbm;
-  } else {
-    L.tw = tw_hbm;
-    L.ej = ej_hbm;
   }
   // pass A, thread per relevant patch: records, edge offsets, patch of each edge
   int* rpo = reinterpret_cast<int*>(L.qu);  // first sorted position (until the first linearisation)
@@ -768,7 +839,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       const unsigned si = wslot((int)gi[r], A.t0, N, fmin), sj = wslot((int)gj[r], A.t0, N, fmin);
       L.ec[q] = (unsigned short)(si | (sj << 8));
       L.eid[q] = ev[r];
-      L.tw[q] = make_float4(tg[r].x, tg[r].y, wt[r].x, wt[r].y);
+      if (L.tw) L.tw[q] = make_float4(tg[r].x, tg[r].y, wt[r].x, wt[r].y);
     }
   }
   // pose table: free poses t0.., then fixed ones from fmin
@@ -812,7 +883,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
         for (int q = L.roff[ri]; q < L.roff[ri + 1]; q++) {
           const unsigned c = L.ec[q];
           const unsigned si = c & 0xff, sj = c >> 8;
-          const float4* e4 = reinterpret_cast<const float4*>(L.ej + 12 * (size_t)q);
+          const float4* e4 = reinterpret_cast<const float4*>(L.ej_at(A.ejg, A.E, q, (it - 1) & 1));
           const float4 e0 = e4[0], e1 = e4[1], e2 = e4[2];
           if (sj < (unsigned)N) {
             const double* d = L.dX + 6 * sj;
@@ -843,12 +914,12 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     double* part = pbuf + (size_t)g * kPartPad;
     double* red = reinterpret_cast<double*>(L.region);
     if (NB == 0) {
-      assemble<0>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, acc);
+      assemble<0>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
     } else if (diag) {
-      assemble<1>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, acc);
+      assemble<1>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
       reduce_acc<27>(acc, red, part);
     } else {
-      assemble<2>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, acc);
+      assemble<2>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
       reduce_acc<36>(acc, red, part);
     }
     mark(A, mb + 0);
@@ -961,7 +1032,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       for (int q = L.roff[ri]; q < L.roff[ri + 1]; q++) {
         const unsigned c = L.ec[q];
         const unsigned si = c & 0xff, sj = c >> 8;
-        const float4* e4 = reinterpret_cast<const float4*>(L.ej + 12 * (size_t)q);
+        const float4* e4 = reinterpret_cast<const float4*>(L.ej_at(A.ejg, A.E, q, (it - 1) & 1));
         const float4 e0 = e4[0], e1 = e4[1], e2 = e4[2];
         if (sj < (unsigned)N) {
           const double* d = L.dX + 6 * sj;
@@ -1027,8 +1098,11 @@ static WGrid window_grid(int E, int N) {
     w.G = 1;
     return w;
   }
-  w.So = E > 2048 ? 2 : 1;
-  w.Sd = 4 * w.So;
+  // shares per block: sparse graphs (cfg2: ~1.8 edges per patch) load the
+  // diagonal blocks most; DPVO windows (a patch sees ~10 free poses) load
+  // every block alike, so large windows split all blocks evenly
+  w.So = E > 2048 ? 4 : 1;
+  w.Sd = 4;
   auto G = [&]() { return N * w.Sd + (w.NB - N) * w.So; };
   while (G() > kWMaxG && w.Sd > 1) {
     if (w.Sd > w.So) w.Sd--;
@@ -1074,7 +1148,7 @@ size_t ba_window_scratch_bytes(int E, int N) {
   return al256w(sizeof(int) * (size_t)E) + al256w(sizeof(int) * (size_t)(E + 1)) +
          al256w(sizeof(unsigned) * (size_t)E) + al256w(sizeof(int) * (size_t)E) +
          al256w(sizeof(int) * 8) + al256w(sizeof(double) * 2 * kPartPad * (size_t)w.G) +
-         al256w(sizeof(float) * 16 * (size_t)w.G * E);
+         al256w(sizeof(float) * 24 * (size_t)E);
 }
 
 namespace {

@@ -136,7 +136,7 @@ size_t dpvo_ba_workspace_bytes(int E, int t0, int t1);
 /* Instrumentation / testing: which F-BA implementation dpvo_ba_forward uses.
    0 = auto: the window kernel (ba_window.hip: plan kernel + one persistent
    workgroup per share of a lower 6x6 block of S, dense solve in every
-   workgroup) for E <= 4096 edges and N <= 16 free poses, the multi-kernel
+   workgroup) for E <= 10240 edges and N <= 16 free poses, the multi-kernel
    path (ba.hip) for E <= 16384 and N <= 20, the large-graph path
    (ba_large.hip) beyond; 2 = the multi-kernel path; 4 = always the
    large-graph path; 5 = same as 0.  1 and 3 (the round-1 single-workgroup
@@ -222,7 +222,7 @@ int dpvo_ba_last_status(const void* workspace, int E, int t0, int t1, int* out, 
    can run on a side stream concurrently with A-CORR -- and
    dpvo_ba_forward_planned runs the iterations on that workspace (same
    workspace size as dpvo_ba_forward; identical results).  Only for shapes
-   dpvo_ba_plan_supported() accepts (the window path: E <= 4096, N <= 16,
+   dpvo_ba_plan_supported() accepts (the window path: E <= 10240, N <= 16,
    P * P <= 64); otherwise call dpvo_ba_forward. */
 int dpvo_ba_plan_supported(int E, int t0, int t1, int P);
 /* Byte offsets, inside a dpvo_ba_plan workspace, of the plan arrays:

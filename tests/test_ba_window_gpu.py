@@ -76,7 +76,7 @@ def test_planned_forward_is_bit_identical(cb, gpu, cfg):
     assert cb.check_status(poses) == 0
 
 
-@pytest.mark.parametrize("cfg", ["cfg1", "cfg2", "dpvo10"])
+@pytest.mark.parametrize("cfg", ["cfg1", "cfg2", "dpvo10", "dpvo25"])
 def test_reproject_plan_fused_is_bit_identical(cb, gpu, cfg):
     """reproject(mem=, plan_window=) (dpvo_reproject_ordered_plan: reprojection,
     A-CORR edge order and BA plan in one launch) == reproject_ordered + plan:
@@ -84,8 +84,9 @@ def test_reproject_plan_fused_is_bit_identical(cb, gpu, cfg):
     BA() bit for bit."""
     from dpvo_amd import fastba
 
-    if cfg == "dpvo10":  # E = 3940: DPVO's edge pattern inside the window path's E <= 4096
-        G = synthetic.make_dpvo_window(M=10, seed=10)
+    if cfg.startswith("dpvo"):  # DPVO's edge pattern: E = 3940 (M = 10) / 9850 (M = 25)
+        m = int(cfg[4:])
+        G = synthetic.make_dpvo_window(M=m, seed=m)
         t0, t1 = G.F - 10, G.F
     else:
         G = synthetic.make_config(cfg, seed=11)
@@ -109,13 +110,26 @@ def test_reproject_plan_fused_is_bit_identical(cb, gpu, cfg):
     assert cb.check_status(poses) == 0
 
 
+def test_window_path_covers_dpvo_max_edges(gpu):
+    """The window path takes every DPVO local-BA window up to MAX_EDGES =
+    10000 (dpvo/config.py:42) with N <= 16 free poses."""
+    from dpvo_amd import fastba
+
+    for E in (3940, 7092, 9850, 10000):
+        assert fastba.cuda_ba.plan_supported(E, 12, 22, 3)
+    assert fastba.cuda_ba.plan_supported(10000, 0, 16, 3)
+    assert not fastba.cuda_ba.plan_supported(10241, 12, 22, 3)
+    assert not fastba.cuda_ba.plan_supported(4000, 0, 17, 3)
+
+
 def test_reproject_plan_fused_unsupported_window_raises(gpu):
-    """Outside the window path (E > 4096) the fused launch reports
+    """Outside the window path (E > 10240) the fused launch reports
     unsupported (as fastba.plan returns None there) and writes nothing."""
     from dpvo_amd import fastba
 
-    G = synthetic.make_dpvo_window(M=18, seed=18)  # E = 7092
+    G = synthetic.make_dpvo_window(M=27, seed=27)  # E > 10240
     D = G.to(gpu)
+    assert D.ii.numel() > 10240
     assert not fastba.cuda_ba.plan_supported(int(D.ii.numel()), G.F - 10, G.F, 3)
     with pytest.raises(RuntimeError, match="unsupported"):
         fastba.reproject(D.poses, D.patches, D.intrinsics, D.ii, D.jj, D.kk, mem=G.F,
@@ -201,13 +215,16 @@ def _plan_arrays(cb, ws, E, t0, t1):
 
 @pytest.mark.parametrize("E,nk,M,seed", [(96, 40, 1024, 0), (700, 650, 1024, 1),
                                          (3000, 2500, 1024, 2), (4096, 300, 1024, 3),
-                                         (4000, 3900, 1024, 4), (2048, 1500, 2048, 5)])
+                                         (4000, 3900, 1024, 4), (2048, 1500, 2048, 5),
+                                         (10000, 9000, 1024, 6), (10240, 550, 1024, 7),
+                                         (6000, 5000, 4096, 8), (9850, 9000, 4096, 9)])
 def test_plan_grouping_matches_host(cb, gpu, E, nk, M, seed):
     """Regression for the plan's counting sort (the head flags of every
     bucket are read before any wave bumps a bucket counter): many small
     buckets and E > 64, through fastba.plan and the fused reprojection launch,
-    the grouping is exactly the host one, on repeated calls.  M = 2048 puts
-    the kk range past the counting sort's (bitonic path)."""
+    the grouping is exactly the host one, on repeated calls.  M = 2048 / 4096
+    put the kk range past the counting sort's (bitonic path: 64-bit keys up
+    to E = 8192, packed 32-bit keys above)."""
     from dpvo_amd import fastba
 
     rng = np.random.default_rng(seed)
