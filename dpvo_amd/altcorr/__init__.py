@@ -5,7 +5,8 @@ Same entry points as dpvo/altcorr/correlation.py of cuteboyqq/DPVO
 HIP extension.  Extra: `corr_levels`, the fused all-levels call of
 DPVO.corr (dpvo/dpvo.py:456-465) in one launch, and `to_channels_last`
 (pyramids stored channels-last take the matrix-core correlation path), and
-`insert_frame`, the one-launch channels-last frame insertion of all levels.
+`insert_frame`, the one-launch channels-last frame insertion of all levels
+(`insert_frame_ring`: ring slot read on the device, for graph replay).
 """
 from .correlation import (  # noqa: F401
     BORDER_MODE,
@@ -14,6 +15,7 @@ from .correlation import (  # noqa: F401
     corr,
     corr_levels,
     insert_frame,
+    insert_frame_ring,
     patchify,
     to_channels_last,
 )

@@ -113,6 +113,14 @@ def insert_frame(fmap, pyramid, slot, scales=(1, 4)):
                                      [int(s) for s in scales])
 
 
+def insert_frame_ring(fmap, pyramid, slot_dev, scales=(1, 4)):
+    """insert_frame with the ring slot read on the device: slot = slot_dev[0] %
+    mem (int32 device scalar), so a captured update graph can be replayed for
+    every new frame."""
+    require_gpu(fmap)
+    cuda_corr.feature_pyramid_insert_ring(fmap, list(pyramid), [int(s) for s in scales], slot_dev)
+
+
 def corr_levels(fmap1, pyramid, coords, ii, jj, radius=3, scales=(1, 4), order=None):
     """DPVO.corr (dpvo/dpvo.py:456-465) in ONE launch: correlation of every
     pyramid level (coords divided by each level's scale) stacked on the last

@@ -1053,16 +1053,19 @@ int ba_window_launch(float* poses, float* patches, const float* intrinsics, cons
                      const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
                      int iterations, char* scratch, int* status, int64_t* marks, void* stream);
 int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
-                   int num_poses, int t0, int t1, char* scratch, int* status, void* stream);
+                   int num_poses, int t0, int t1, char* scratch, int* status, void* stream,
+                   const int* t0d);
 void ba_window_plan_offsets(int E, int64_t* out);
 int ba_window_reproject_plan(const float* poses, const float* patches, const float* intrinsics,
                              const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int P,
                              int num_poses, int num_patches, int N2, float* coords, int* order,
-                             int t0, int t1, char* scratch, int* status, void* stream);
+                             int t0, int t1, char* scratch, int* status, void* stream,
+                             const int* t0d);
 int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
                   const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                   const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
-                  int iterations, char* scratch, int* status, int64_t* marks, void* stream);
+                  int iterations, char* scratch, int* status, int64_t* marks, void* stream,
+                  const int* t0d);
 // ba_large.hip: large graphs (global BA, cfg4)
 size_t gba_workspace_bytes(int E, int N);
 int gba_forward(float* poses, float* patches, const float* intrinsics, const float* target,
@@ -1357,7 +1360,7 @@ DPVO_EXPORT int dpvo_ba_plan(const int64_t* ii, const int64_t* jj, const int64_t
   BaWs w;
   const size_t base_bytes = ba_layout(E, t1 - t0, (char*)workspace, &w);
   return ba_window_plan(ii, jj, kk, E, num_patches, num_poses, t0, t1,
-                        (char*)workspace + base_bytes, w.meta + 1, stream);
+                        (char*)workspace + base_bytes, w.meta + 1, stream, nullptr);
 }
 
 DPVO_EXPORT int dpvo_ba_forward_planned(float* poses, float* patches, const float* intrinsics,
@@ -1376,7 +1379,27 @@ DPVO_EXPORT int dpvo_ba_forward_planned(float* poses, float* patches, const floa
   const size_t base_bytes = ba_layout(E, t1 - t0, (char*)workspace, &w);
   return ba_window_run(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
                        num_poses, num_patches, t0, t1, iterations, (char*)workspace + base_bytes,
-                       w.meta + 1, w.tmark, stream);
+                       w.meta + 1, w.tmark, stream, nullptr);
+}
+
+DPVO_EXPORT int dpvo_ba_forward_planned_dev(float* poses, float* patches, const float* intrinsics,
+                                            const float* target, const float* weight,
+                                            const float* lmbda, const int64_t* ii,
+                                            const int64_t* jj, const int64_t* kk, int E, int P,
+                                            int num_poses, int num_patches, const int32_t* t0_dev,
+                                            int N, int iterations, void* workspace,
+                                            size_t workspace_bytes, void* stream) {
+  if (E <= 0 || iterations <= 0) return DPVO_OK;
+  if (P < 2 || num_poses <= 0 || num_patches <= 0 || N < 0 || !t0_dev || !workspace || !poses ||
+      !patches || !intrinsics || !target || !weight || !lmbda || !ii || !jj || !kk)
+    return DPVO_ERR_INVALID;
+  if (!ba_window_supported(E, N, P)) return DPVO_ERR_UNSUPPORTED;
+  if (workspace_bytes < dpvo_ba_workspace_bytes(E, 0, N)) return DPVO_ERR_WORKSPACE;
+  BaWs w;
+  const size_t base_bytes = ba_layout(E, N, (char*)workspace, &w);
+  return ba_window_run(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
+                       num_poses, num_patches, 0, N, iterations, (char*)workspace + base_bytes,
+                       w.meta + 1, w.tmark, stream, t0_dev);
 }
 
 DPVO_EXPORT int dpvo_reproject(const float* poses, const float* patches, const float* intrinsics,
@@ -1422,7 +1445,27 @@ DPVO_EXPORT int dpvo_reproject_ordered_plan(const float* poses, const float* pat
   const size_t base_bytes = ba_layout(E, t1 - t0, (char*)workspace, &w);
   return ba_window_reproject_plan(poses, patches, intrinsics, ii, jj, kk, E, P, num_poses,
                                   num_patches, N2, coords, (int*)order, t0, t1,
-                                  (char*)workspace + base_bytes, w.meta + 1, stream);
+                                  (char*)workspace + base_bytes, w.meta + 1, stream, nullptr);
+}
+
+DPVO_EXPORT int dpvo_reproject_ordered_plan_dev(const float* poses, const float* patches,
+                                                const float* intrinsics, const int64_t* ii,
+                                                const int64_t* jj, const int64_t* kk, int E, int P,
+                                                int num_poses, int num_patches, int N2,
+                                                float* coords, int32_t* order,
+                                                const int32_t* t0_dev, int N, void* workspace,
+                                                size_t workspace_bytes, void* stream) {
+  if (E <= 0) return DPVO_OK;
+  if (P <= 0 || num_poses <= 0 || num_patches <= 0 || !order || !coords || !poses || !patches ||
+      !intrinsics || !ii || !jj || !kk || !workspace || !t0_dev || N < 0)
+    return DPVO_ERR_INVALID;
+  if (!ba_window_supported(E, N, P)) return DPVO_ERR_UNSUPPORTED;
+  if (workspace_bytes < dpvo_ba_workspace_bytes(E, 0, N)) return DPVO_ERR_WORKSPACE;
+  BaWs w;
+  const size_t base_bytes = ba_layout(E, N, (char*)workspace, &w);
+  return ba_window_reproject_plan(poses, patches, intrinsics, ii, jj, kk, E, P, num_poses,
+                                  num_patches, N2, coords, (int*)order, 0, N,
+                                  (char*)workspace + base_bytes, w.meta + 1, stream, t0_dev);
 }
 
 DPVO_EXPORT int dpvo_neighbors_max_edges(void) { return 1 << 30; }

@@ -69,6 +69,7 @@ struct Plan {          // written by ba_plan_kernel, read by ba_window_kernel
   int* meta;           // [8] nuniq, fmin, status
   int* status;         // the workspace status word, reset here
   int* sink;           // caller's sticky status word or null
+  const int* t0d;      // device t0 (graph-replayed updates: t0 moves per frame) or null
 };
 
 struct WArgs {
@@ -89,6 +90,7 @@ struct WArgs {
   int* status;       // [1] OR of status bits (workspace meta)
   int* sink;         // caller's sticky status word (dpvo_ba_set_status_sink) or null
   int64_t* marks;    // [64] wall-clock stamps of workgroup 0 (may be null)
+  const int* t0d;    // device t0 or null (then t0)
 };
 
 __device__ __forceinline__ size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -131,6 +133,7 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
                                            const int64_t* __restrict__ kk, int E, int num_patches,
                                            int num_poses, int t0, int N, const Plan& plan,
                                            char* lds) {
+  if (plan.t0d) t0 = *plan.t0d;
   // LDS (153.9 KB at kWMaxE = 10240): per-edge arrays as u16 / u8, one union
   //   [ctl 256 B | code u16[E] | key u16[E] -> ranked | spos u16[E] | head u8[E] | U 80 KB]
   //   U: counting sort hist int[kHistMax], later hd int[E] + mask u32[E];
@@ -648,6 +651,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   const bool diag = (a == b);
   const float fx = A.intrinsics[0], fy = A.intrinsics[1], cx = A.intrinsics[2],
               cy = A.intrinsics[3];
+  const int t0w = A.t0d ? *A.t0d : A.t0;  // first free pose
   // this call's tag: every workgroup reads it at entry; workgroup 0 advances it
   // at its very end, after everyone has read it: each workgroup's read is
   // program-ordered before its RELEASED iteration-0 flag, which workgroup 0
@@ -836,7 +840,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     for (int r = 0; r < kB; r++) {
       const int q = q0 + r * kWT;
       if (q >= nrp) continue;
-      const unsigned si = wslot((int)gi[r], A.t0, N, fmin), sj = wslot((int)gj[r], A.t0, N, fmin);
+      const unsigned si = wslot((int)gi[r], t0w, N, fmin), sj = wslot((int)gj[r], t0w, N, fmin);
       L.ec[q] = (unsigned short)(si | (sj << 8));
       L.eid[q] = ev[r];
       if (L.tw) L.tw[q] = make_float4(tg[r].x, tg[r].y, wt[r].x, wt[r].y);
@@ -849,7 +853,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
 #pragma unroll
     for (int r = 0; r < kPr; r++) {
       const int k = tid + r * kWT, sl = k >> 3, c = k & 7;
-      const int gp = (sl < N) ? A.t0 + sl : fmin + (sl - N);
+      const int gp = (sl < N) ? t0w + sl : fmin + (sl - N);
       pv[r] = (c == 6) ? 1.0f : 0.0f;
       if (c < 7 && gp >= 0 && gp < A.num_poses && (sl < N || fmin != 0x7fffffff))
         pv[r] = A.poses[7 * (size_t)gp + c];
@@ -1060,7 +1064,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     }
     if (g == 0)
       for (int i = tid; i < N; i += kWT) {
-        const int gp = A.t0 + i;
+        const int gp = t0w + i;
         if (gp >= 0 && gp < A.num_poses)
           for (int c = 0; c < 7; c++) A.poses[7 * (size_t)gp + c] = L.pose[8 * i + c];
       }
@@ -1210,6 +1214,7 @@ static Plan plan_view(char* scratch, int E, int* status) {
   p.meta = (int*)s;
   p.status = status;
   p.sink = sink_for_device();
+  p.t0d = nullptr;
   return p;
 }
 
@@ -1229,9 +1234,11 @@ static void set_attrs() {
 // edge grouping only (reads ii / jj / kk): may run on another stream than
 // the iterations, e.g. concurrently with A-CORR
 int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
-                   int num_poses, int t0, int t1, char* scratch, int* status, void* stream) {
+                   int num_poses, int t0, int t1, char* scratch, int* status, void* stream,
+                   const int* t0d) {
   set_attrs();
-  const Plan plan = plan_view(scratch, E, status);
+  Plan plan = plan_view(scratch, E, status);
+  plan.t0d = t0d;
   hipLaunchKernelGGL(ba_plan_kernel, dim3(1), dim3(kPT), kWLds, as_stream(stream), ii, jj, kk, E,
                      num_patches, num_poses, t0, t1 - t0, plan);
   return launch_status();
@@ -1242,9 +1249,11 @@ int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int 
 int ba_window_reproject_plan(const float* poses, const float* patches, const float* intrinsics,
                              const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int P,
                              int num_poses, int num_patches, int N2, float* coords, int* order,
-                             int t0, int t1, char* scratch, int* status, void* stream) {
+                             int t0, int t1, char* scratch, int* status, void* stream,
+                             const int* t0d) {
   set_attrs();
-  const Plan plan = plan_view(scratch, E, status);
+  Plan plan = plan_view(scratch, E, status);
+  plan.t0d = t0d;
   RArgs r;
   r.poses = poses;
   r.patches = patches;
@@ -1270,14 +1279,15 @@ int ba_window_reproject_plan(const float* poses, const float* patches, const flo
 int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
                   const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                   const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
-                  int iterations, char* scratch, int* status, int64_t* marks, void* stream);
+                  int iterations, char* scratch, int* status, int64_t* marks, void* stream,
+                  const int* t0d = nullptr);
 
 int ba_window_launch(float* poses, float* patches, const float* intrinsics, const float* target,
                      const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                      const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
                      int iterations, char* scratch, int* status, int64_t* marks, void* stream) {
   const int rc = ba_window_plan(ii, jj, kk, E, num_patches, num_poses, t0, t1, scratch, status,
-                                stream);
+                                stream, nullptr);
   if (rc) return rc;
   return ba_window_run(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
                        num_poses, num_patches, t0, t1, iterations, scratch, status, marks, stream);
@@ -1286,7 +1296,8 @@ int ba_window_launch(float* poses, float* patches, const float* intrinsics, cons
 int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
                   const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                   const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
-                  int iterations, char* scratch, int* status, int64_t* marks, void* stream) {
+                  int iterations, char* scratch, int* status, int64_t* marks, void* stream,
+                  const int* t0d) {
   set_attrs();
   if (iterations > 63) return DPVO_ERR_UNSUPPORTED;  // 6-bit iteration tag per epoch
   const int N = t1 - t0;
@@ -1316,6 +1327,7 @@ int ba_window_run(float* poses, float* patches, const float* intrinsics, const f
   a.num_poses = num_poses;
   a.num_patches = num_patches;
   a.t0 = t0;
+  a.t0d = t0d;
   a.N = N;
   a.iters = iterations;
   a.NB = w.NB;

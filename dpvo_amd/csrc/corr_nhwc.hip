@@ -596,6 +596,11 @@ constexpr int kInsCS = kInsTY * kInsTX + 1;  // channel stride (+1: no bank conf
 struct InsLevels {
   void* dst[kMaxL];  // float or __half (the source's dtype)
   int s[kMaxL];
+  // ring variant (graph-replayed frames): dst[l] is slot 0 of level l, the
+  // slot is *slot_dev % mem, slots slot_bytes[l] apart; null = dst as given
+  const int* slot_dev;
+  int mem;
+  long long slot_bytes[kMaxL];
 };
 
 // level-1 copy of the LDS tile: one float4 (4 channels) per lane, 8 lanes per
@@ -716,8 +721,9 @@ __global__ void __launch_bounds__(256)
   }
   __syncthreads();
   // level 1: one float4 (4 channels) per lane, 8 lanes per pixel = one 128-B run
+  const long long slot = lv.slot_dev ? (long long)(((*lv.slot_dev) % lv.mem + lv.mem) % lv.mem) : 0;
   for (int l = 0; l < L; l++) {
-    T* d = static_cast<T*>(lv.dst[l]);
+    T* d = reinterpret_cast<T*>(static_cast<char*>(lv.dst[l]) + slot * lv.slot_bytes[l]);
     switch (lv.s[l]) {
       case 1: ins_copy(tile, d, tx0, ty0, c0, C, H, W, tid); break;
       case 2: ins_pool<2>(tile, d, tx0, ty0, c0, C, H, W, tid); break;
@@ -816,11 +822,16 @@ DPVO_EXPORT int dpvo_feature_to_nhwc(const void* src, void* dst, int count, int 
   return DPVO_ERR_UNSUPPORTED;
 }
 
-DPVO_EXPORT int dpvo_feature_pyramid_insert(const void* src, void* const* dst, const int* scale,
-                                            int L, int C, int H, int W, int dtype, void* stream) {
+static int pyramid_insert_impl(const void* src, void* const* dst, const int* scale, int L, int C,
+                               int H, int W, int dtype, void* stream, const int32_t* slot_dev,
+                               int mem, const int64_t* slot_bytes) {
   if (!src || !dst || !scale || L <= 0 || C <= 0 || H <= 0 || W <= 0) return DPVO_ERR_INVALID;
   if ((dtype != DPVO_F32 && dtype != DPVO_F16) || L > kMaxL) return DPVO_ERR_UNSUPPORTED;
+  if (slot_dev && (mem <= 0 || !slot_bytes)) return DPVO_ERR_INVALID;
   InsLevels lv = {};
+  lv.slot_dev = (const int*)slot_dev;
+  lv.mem = mem > 0 ? mem : 1;
+  for (int l = 0; l < L && slot_dev; l++) lv.slot_bytes[l] = slot_bytes[l];
   for (int l = 0; l < L; l++) {
     const int s = scale[l];
     if (!dst[l]) return DPVO_ERR_INVALID;
@@ -836,4 +847,18 @@ DPVO_EXPORT int dpvo_feature_pyramid_insert(const void* src, void* const* dst, c
     hipLaunchKernelGGL(pyramid_insert_kernel<float>, grid, dim3(256), 0, as_stream(stream),
                        (const float*)src, lv, L, C, H, W);
   return launch_status();
+}
+
+DPVO_EXPORT int dpvo_feature_pyramid_insert(const void* src, void* const* dst, const int* scale,
+                                            int L, int C, int H, int W, int dtype, void* stream) {
+  return pyramid_insert_impl(src, dst, scale, L, C, H, W, dtype, stream, nullptr, 0, nullptr);
+}
+
+DPVO_EXPORT int dpvo_feature_pyramid_insert_ring(const void* src, void* const* dst0,
+                                                 const int64_t* slot_bytes, const int* scale,
+                                                 int L, int C, int H, int W, int mem,
+                                                 const int32_t* slot_dev, int dtype, void* stream) {
+  if (!slot_dev) return DPVO_ERR_INVALID;
+  return pyramid_insert_impl(src, dst0, scale, L, C, H, W, dtype, stream, slot_dev, mem,
+                             slot_bytes);
 }

@@ -351,6 +351,76 @@ std::vector<torch::Tensor> ba_reproject_ordered_plan(torch::Tensor poses, torch:
   return {coords.view({1, E, 2, P, P}), order, ws};
 }
 
+// Device-t0 variants (graph-replayed DPVO updates: the window start moves
+// every frame while shapes stay fixed): t0_dev is an int32 device scalar, N =
+// t1 - t0 the (fixed) number of free poses.
+static const int32_t* dev_scalar(const torch::Tensor& t, const char* name) {
+  check_device(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kInt32 && t.numel() >= 1 && t.is_contiguous(), name,
+              " must be a contiguous int32 device tensor");
+  return t.data_ptr<int32_t>();
+}
+
+std::vector<torch::Tensor> ba_reproject_ordered_plan_dev(torch::Tensor poses, torch::Tensor patches,
+                                                         torch::Tensor intrinsics, torch::Tensor ii,
+                                                         torch::Tensor jj, torch::Tensor kk, int N2,
+                                                         torch::Tensor t0_dev, int N) {
+  poses = f32_contig(poses, "poses");
+  patches = f32_contig(patches, "patches");
+  intrinsics = f32_contig(intrinsics, "intrinsics");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  kk = idx64(kk, "kk");
+  const int P = patches.size(-1);
+  const int E = ii.numel();
+  TORCH_CHECK(jj.numel() == E && kk.numel() == E, "ii, jj, kk must have equal length");
+  auto coords = torch::empty({E, 2, P, P}, poses.options());
+  auto order = torch::empty({E}, poses.options().dtype(torch::kInt32));
+  const size_t wsb = dpvo_ba_workspace_bytes(E, 0, N);
+  auto ws = torch::empty({(int64_t)wsb}, poses.options().dtype(torch::kUInt8));
+  check_status(dpvo_reproject_ordered_plan_dev(
+                   poses.data_ptr<float>(), patches.data_ptr<float>(), intrinsics.data_ptr<float>(),
+                   ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), kk.data_ptr<int64_t>(), E, P,
+                   poses.numel() / 7, patches.numel() / (3 * P * P), N2, coords.data_ptr<float>(),
+                   order.data_ptr<int32_t>(), dev_scalar(t0_dev, "t0_dev"), N, ws.data_ptr(), wsb,
+                   current_stream()),
+               "cuda_ba.reproject_ordered_plan_dev");
+  return {coords.view({1, E, 2, P, P}), order, ws};
+}
+
+void ba_forward_planned_dev(torch::Tensor ws, torch::Tensor poses, torch::Tensor patches,
+                            torch::Tensor intrinsics, torch::Tensor target, torch::Tensor weight,
+                            torch::Tensor lmbda, torch::Tensor ii, torch::Tensor jj,
+                            torch::Tensor kk, torch::Tensor t0_dev, int N, int iterations) {
+  check_device(poses, "poses");
+  check_device(patches, "patches");
+  TORCH_CHECK(poses.scalar_type() == torch::kFloat32 && patches.scalar_type() == torch::kFloat32,
+              "poses / patches must be float32");
+  TORCH_CHECK(poses.is_contiguous() && patches.is_contiguous(),
+              "poses and patches must be contiguous (updated in place)");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  const int P = patches.size(-1);
+  intrinsics = f32_contig(intrinsics, "intrinsics");
+  target = f32_contig(target, "target");
+  weight = f32_contig(weight, "weight");
+  lmbda = f32_contig(lmbda, "lmbda");
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  kk = idx64(kk, "kk");
+  const int E = ii.numel();
+  TORCH_CHECK(jj.numel() == E && kk.numel() == E && target.numel() == 2 * (int64_t)E &&
+                  weight.numel() == 2 * (int64_t)E,
+              "ii / jj / kk / target / weight sizes disagree");
+  check_status(dpvo_ba_forward_planned_dev(
+                   poses.data_ptr<float>(), patches.data_ptr<float>(), intrinsics.data_ptr<float>(),
+                   target.data_ptr<float>(), weight.data_ptr<float>(), lmbda.data_ptr<float>(),
+                   ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), kk.data_ptr<int64_t>(), E, P,
+                   poses.numel() / 7, patches.numel() / (3 * P * P), dev_scalar(t0_dev, "t0_dev"),
+                   N, iterations, ws.data_ptr(), ws.numel(), current_stream()),
+               "cuda_ba.forward_planned_dev");
+}
+
 // ba.cpp:59-97 (host loop in the reference; here one O(E^2) LDS-tiled kernel)
 std::vector<torch::Tensor> ba_neighbors(torch::Tensor ii, torch::Tensor jj) {
   ii = idx64(ii, "ii");
@@ -652,6 +722,28 @@ void pg_remove(c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> i
                "cuda_ba.pg_remove");
 }
 
+void pg_remove_window_dev(torch::Tensor ix, torch::Tensor n_dev, int64_t thresh_off,
+                         int64_t lc_off, bool lc_on, bool store, std::vector<torch::Tensor> act,
+                         std::vector<torch::Tensor> back, std::vector<torch::Tensor> inac,
+                         torch::Tensor counts, torch::Tensor pos) {
+  TORCH_CHECK(act.size() == 6 && back.size() == 6 && inac.size() == 5,
+              "act/back: [ii, jj, kk, net, weight, target]; inac: [ii, jj, kk, weight, target]");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(counts.device());
+  const int max_edges = act[0].numel();
+  const int DIM = act[3].defined() && act[3].numel() ? (int)(act[3].numel() / max_edges) : 0;
+  ix = idx64(ix, "ix");
+  auto L = [](const torch::Tensor& t) { return t.data_ptr<int64_t>(); };
+  check_status(dpvo_pg_remove_window_dev(
+                   ix.data_ptr<int64_t>(), dev_scalar(n_dev, "n_dev"), thresh_off, lc_off,
+                   lc_on ? 1 : 0, store ? 1 : 0, L(act[0]), L(act[1]), L(act[2]), opt_f32(act[3]),
+                   act[4].data_ptr<float>(), act[5].data_ptr<float>(), L(back[0]), L(back[1]),
+                   L(back[2]), opt_f32(back[3]), back[4].data_ptr<float>(),
+                   back[5].data_ptr<float>(), L(inac[0]), L(inac[1]), L(inac[2]),
+                   inac[3].data_ptr<float>(), inac[4].data_ptr<float>(), DIM,
+                   counts.data_ptr<int>(), pos.data_ptr<int>(), max_edges, current_stream()),
+               "cuda_ba.pg_remove_window_dev");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("forward", &ba_forward, "BA forward operator");
   m.def("neighbors", &ba_neighbors, "temporal neighboor indicies");
@@ -682,6 +774,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("forward_marks", &ba_forward_marks, "forward + per-phase wall-clock marks");
   m.def("reproject_ordered_plan", &ba_reproject_ordered_plan,
         "reproject + A-CORR edge order + BA plan (workspace for forward_planned), one launch");
+  m.def("reproject_ordered_plan_dev", &ba_reproject_ordered_plan_dev,
+        "reproject_ordered_plan with the window start t0 read from an int32 device scalar");
+  m.def("forward_planned_dev", &ba_forward_planned_dev,
+        "forward_planned with t0 read from an int32 device scalar (graph replay)");
+  m.def("pg_remove_window_dev", &pg_remove_window_dev,
+        "DPVO.keyframe window removal with thresholds relative to a device frame count");
   m.def("reproject_ordered", &ba_reproject_ordered,
         "reproject + edge order by target frame (for cuda_corr.forward_levels(order=))");
   m.def("select_path", [](int mode) { check_status(dpvo_ba_select_path(mode), "select_path"); },

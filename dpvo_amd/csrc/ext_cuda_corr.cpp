@@ -93,6 +93,46 @@ void feature_pyramid_insert(torch::Tensor src, std::vector<torch::Tensor> dst,
                "cuda_corr.feature_pyramid_insert");
 }
 
+// ring variant: slot = *slot_dev % mem read on the device (graph-replayed
+// frames); rings[l] is the whole [B, mem, C, H/s, W/s] channels-last ring
+void feature_pyramid_insert_ring(torch::Tensor src, std::vector<torch::Tensor> rings,
+                                 std::vector<int64_t> scales, torch::Tensor slot_dev) {
+  check_device(src, "src");
+  check_device(slot_dev, "slot_dev");
+  TORCH_CHECK(slot_dev.scalar_type() == torch::kInt32 && slot_dev.is_contiguous(),
+              "slot_dev must be a contiguous int32 device tensor");
+  TORCH_CHECK(src.dim() == 3, "src must be [C, H, W]");
+  TORCH_CHECK(rings.size() == scales.size() && !rings.empty(), "one scale per ring level");
+  TORCH_CHECK(src.scalar_type() == torch::kFloat32 || src.scalar_type() == torch::kFloat16,
+              "src must be float32 or float16");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(src.device());
+  src = src.contiguous();
+  const int C = src.size(0), H = src.size(1), W = src.size(2);
+  const int mem = rings[0].size(1);
+  std::vector<void*> ptrs;
+  std::vector<int64_t> slot_bytes;
+  std::vector<int> sc;
+  for (size_t l = 0; l < rings.size(); l++) {
+    const torch::Tensor d = rings[l][0][0];  // slot 0 of the ring
+    check_device(d, "ring");
+    const int s = (int)scales[l];
+    TORCH_CHECK(rings[l].dim() == 5 && rings[l].size(1) == mem, "rings must be [B, mem, C, h, w]");
+    TORCH_CHECK(d.scalar_type() == src.scalar_type() && d.size(0) == C && s > 0 &&
+                    d.size(1) == H / s && d.size(2) == W / s,
+                "ring level ", l, " must be [C, H/s, W/s] of src's dtype");
+    TORCH_CHECK(d.stride(0) == 1 && d.stride(2) == C && d.stride(1) == (int64_t)C * d.size(2),
+                "ring level ", l, " must be channels-last");
+    ptrs.push_back(d.data_ptr());
+    slot_bytes.push_back(rings[l].stride(1) * (int64_t)rings[l].element_size());
+    sc.push_back(s);
+  }
+  check_status(dpvo_feature_pyramid_insert_ring(src.data_ptr(), ptrs.data(), slot_bytes.data(),
+                                                sc.data(), (int)ptrs.size(), C, H, W, mem,
+                                                slot_dev.data_ptr<int32_t>(), dtype_code(src),
+                                                current_stream()),
+               "cuda_corr.feature_pyramid_insert_ring");
+}
+
 torch::Tensor corr_forward_levels(torch::Tensor fmap1, std::vector<torch::Tensor> fmap2,
                                   torch::Tensor coords, torch::Tensor ii, torch::Tensor jj,
                                   int radius, std::vector<double> scales,
@@ -250,6 +290,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("forward_levels", &corr_forward_levels, "CORR forward, all pyramid levels in one launch",
         py::arg("fmap1"), py::arg("fmap2"), py::arg("coords"), py::arg("ii"), py::arg("jj"),
         py::arg("radius"), py::arg("scales"), py::arg("order") = py::none());
+  m.def("feature_pyramid_insert_ring", &feature_pyramid_insert_ring,
+        "feature_pyramid_insert into ring slot *slot_dev % mem (device scalar, graph replay)");
   m.def("feature_pyramid_insert", &feature_pyramid_insert,
         "NCHW level-1 frame -> channels-last pyramid slot (all levels, one launch)");
   m.def("feature_to_nhwc", &feature_to_nhwc, "[..., C, H, W] -> channels-last copy into dst");

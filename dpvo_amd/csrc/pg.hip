@@ -63,9 +63,17 @@ __global__ void pg_count_kernel(int* counts, int n, int max_edges) {
 // flag source: mask (uint8, 1 = remove) or, when mask is null, the DPVO
 // window rule ix[kk] < thresh (dpvo.py:684) except loop-closure edges
 // (jj - ii > 30 and jj > lc_min, dpvo.py:685-688) when lc_min >= 0.
+// n_dev (graph-replayed frames): thresh / lc_min are offsets from the device
+// frame count *n_dev, lc_min only if lc_on.
 __global__ void __launch_bounds__(kPgT) pg_plan_remove_kernel(
     const uint8_t* __restrict__ mask, const int64_t* __restrict__ ix, int64_t thresh,
-    int64_t lc_min, PgBufs a, int* counts, int* __restrict__ pos, int store, int max_edges) {
+    int64_t lc_min, PgBufs a, int* counts, int* __restrict__ pos, int store, int max_edges,
+    const int* n_dev, int lc_on) {
+  if (n_dev) {
+    const int64_t n = *n_dev;
+    thresh += n;
+    lc_min = lc_on ? lc_min + n : -1;
+  }
   __shared__ int wsum[kPgT / 64 + 1];
   __shared__ int carry[2];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -204,13 +212,13 @@ DPVO_EXPORT int dpvo_pg_append(const int64_t* ix, const int64_t* kk_new, const i
   return launch_status();
 }
 
-DPVO_EXPORT int dpvo_pg_remove(const uint8_t* mask, const int64_t* ix, int64_t thresh,
-                               int64_t lc_min, int store, int64_t* ii, int64_t* jj, int64_t* kk,
-                               float* net, float* weight, float* target, int64_t* ii_b,
-                               int64_t* jj_b, int64_t* kk_b, float* net_b, float* weight_b,
-                               float* target_b, int64_t* ii_i, int64_t* jj_i, int64_t* kk_i,
-                               float* weight_i, float* target_i, int DIM, int* counts, int* pos,
-                               int max_edges, void* stream) {
+static int pg_remove_impl(const uint8_t* mask, const int64_t* ix, int64_t thresh, int64_t lc_min,
+                          int store, int64_t* ii, int64_t* jj, int64_t* kk, float* net,
+                          float* weight, float* target, int64_t* ii_b, int64_t* jj_b,
+                          int64_t* kk_b, float* net_b, float* weight_b, float* target_b,
+                          int64_t* ii_i, int64_t* jj_i, int64_t* kk_i, float* weight_i,
+                          float* target_i, int DIM, int* counts, int* pos, int max_edges,
+                          void* stream, const int32_t* n_dev, int lc_on) {
   if (!ii || !jj || !kk || !weight || !target || !ii_b || !jj_b || !kk_b || !weight_b ||
       !target_b || !counts || !pos || max_edges <= 0 || (!mask && !ix) || (net && !net_b) ||
       (net && (DIM <= 0 || DIM % 4)) || (store && (!ii_i || !jj_i || !kk_i || !weight_i || !target_i)))
@@ -220,7 +228,7 @@ DPVO_EXPORT int dpvo_pg_remove(const uint8_t* mask, const int64_t* ix, int64_t t
   const PgBufs b = bufs(ii_b, jj_b, kk_b, net_b, weight_b, target_b);
   const PgBufs in = bufs(ii_i, jj_i, kk_i, nullptr, weight_i, target_i);
   hipLaunchKernelGGL(pg_plan_remove_kernel, dim3(1), dim3(kPgT), 0, st, mask, ix, thresh, lc_min,
-                     a, counts, pos, store, max_edges);
+                     a, counts, pos, store, max_edges, (const int*)n_dev, lc_on);
   int rc = launch_status();
   if (rc) return rc;
   const int64_t work = net ? (int64_t)max_edges * (DIM / 4) : max_edges;
@@ -231,4 +239,30 @@ DPVO_EXPORT int dpvo_pg_remove(const uint8_t* mask, const int64_t* ix, int64_t t
   if (rc) return rc;
   hipLaunchKernelGGL(pg_commit_kernel, dim3(1), dim3(64), 0, st, counts);
   return launch_status();
+}
+
+DPVO_EXPORT int dpvo_pg_remove(const uint8_t* mask, const int64_t* ix, int64_t thresh,
+                               int64_t lc_min, int store, int64_t* ii, int64_t* jj, int64_t* kk,
+                               float* net, float* weight, float* target, int64_t* ii_b,
+                               int64_t* jj_b, int64_t* kk_b, float* net_b, float* weight_b,
+                               float* target_b, int64_t* ii_i, int64_t* jj_i, int64_t* kk_i,
+                               float* weight_i, float* target_i, int DIM, int* counts, int* pos,
+                               int max_edges, void* stream) {
+  return pg_remove_impl(mask, ix, thresh, lc_min, store, ii, jj, kk, net, weight, target, ii_b,
+                        jj_b, kk_b, net_b, weight_b, target_b, ii_i, jj_i, kk_i, weight_i,
+                        target_i, DIM, counts, pos, max_edges, stream, nullptr, 0);
+}
+
+DPVO_EXPORT int dpvo_pg_remove_window_dev(const int64_t* ix, const int32_t* n_dev, int64_t thresh_off,
+                                          int64_t lc_off, int lc_on, int store, int64_t* ii,
+                                          int64_t* jj, int64_t* kk, float* net, float* weight,
+                                          float* target, int64_t* ii_b, int64_t* jj_b,
+                                          int64_t* kk_b, float* net_b, float* weight_b,
+                                          float* target_b, int64_t* ii_i, int64_t* jj_i,
+                                          int64_t* kk_i, float* weight_i, float* target_i, int DIM,
+                                          int* counts, int* pos, int max_edges, void* stream) {
+  if (!n_dev || !ix) return DPVO_ERR_INVALID;
+  return pg_remove_impl(nullptr, ix, thresh_off, lc_off, store, ii, jj, kk, net, weight, target,
+                        ii_b, jj_b, kk_b, net_b, weight_b, target_b, ii_i, jj_i, kk_i, weight_i,
+                        target_i, DIM, counts, pos, max_edges, stream, n_dev, lc_on);
 }

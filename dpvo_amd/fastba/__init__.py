@@ -10,6 +10,8 @@ ii, jj, kk)` -> [1, E, 2, P, P].
 """
 from __future__ import annotations
 
+import torch
+
 from .._native import load_extension
 
 cuda_ba = load_extension("cuda_ba")
@@ -22,12 +24,38 @@ def BA(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, M,
     workspace from :func:`plan` for the same ii / jj / kk / t0 / t1 (the edge
     grouping then is not redone here)."""
     data = poses.data if hasattr(poses, "data") else poses
+    # the fork's MIXED_PRECISION patch graph holds target / weight in fp16
+    # (patchgraph.py:46-52 with autocast kwargs); the kernels read fp32, so the
+    # global-BA call of dpvo.py:695-715 gets fp32 copies here (SURVEY 5: with
+    # fp16 buffers the fork's own global BA never runs)
+    if target.dtype != torch.float32:
+        target = target.float()
+    if weight.dtype != torch.float32:
+        weight = weight.float()
     if plan is not None:
         cuda_ba.forward_planned(plan, data, patches, intrinsics, target, weight, lmbda, ii, jj, kk,
                                 t0, t1, iterations)
         return []
     return cuda_ba.forward(data, patches, intrinsics, target, weight, lmbda, ii, jj, kk, M, t0, t1,
                            iterations, eff_impl)
+
+
+def BA_dev(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0_dev, N, plan,
+           iterations=1):
+    """BA on a planned workspace with the window start t0 read from an int32
+    device scalar (``t0_dev``) and N = t1 - t0 free poses: graph-replayed
+    updates, where t0 moves every frame (same results as BA(plan=...))."""
+    data = poses.data if hasattr(poses, "data") else poses
+    cuda_ba.forward_planned_dev(plan, data, patches, intrinsics, target.float(), weight.float(),
+                                lmbda, ii, jj, kk, t0_dev, int(N), int(iterations))
+    return []
+
+
+def reproject_window_dev(poses, patches, intrinsics, ii, jj, kk, mem, t0_dev, N):
+    """reproject(..., mem, plan_window=(t0, t0 + N)) with t0 read from an int32
+    device scalar: coords, A-CORR edge order and the BA plan in one launch."""
+    return tuple(cuda_ba.reproject_ordered_plan_dev(poses, patches, intrinsics, ii, jj, kk,
+                                                    int(mem), t0_dev, int(N)))
 
 
 def plan(ii, jj, kk, t0, t1, num_patches, num_poses, P=3):
@@ -67,4 +95,4 @@ def reproject(poses, patches, intrinsics, ii, jj, kk, mem=None, plan_window=None
     return tuple(cuda_ba.reproject_ordered(poses, patches, intrinsics, ii, jj, kk, int(mem)))
 
 
-__all__ = ["BA", "plan", "neighbors", "reproject", "cuda_ba"]
+__all__ = ["BA", "BA_dev", "plan", "neighbors", "reproject", "reproject_window_dev", "cuda_ba"]

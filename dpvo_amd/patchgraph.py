@@ -101,5 +101,18 @@ class DevicePatchGraph:
         lc_min = n - optimization_window if loop_closure else -1
         self._remove(None, ix, n - removal_window, lc_min, store)
 
+    def remove_by_window_dev(self, ix, n_dev, removal_window, loop_closure=False,
+                             optimization_window=10, store=True):
+        """remove_by_window with the frame count read on the device (int32
+        scalar n_dev): graph-replayable, the thresholds move with the frame."""
+        a, b = self._a, self._b
+        keys = ("ii", "jj", "kk", "net", "weight", "target")
+        self._ext.pg_remove_window_dev(ix, n_dev, -int(removal_window), -int(optimization_window),
+                                       bool(loop_closure), bool(store), [a[k] for k in keys],
+                                       [b[k] for k in keys],
+                                       [self.ii_inac, self.jj_inac, self.kk_inac, self.weight_inac,
+                                        self.target_inac], self.counts, self._pos)
+        self._a, self._b = b, a
+
 
 __all__ = ["DevicePatchGraph"]

@@ -103,6 +103,13 @@ int dpvo_feature_to_nhwc(const void* src, void* dst, int count, int C, int H, in
    s^2 (torch avg_pool2d order: bit-identical). */
 int dpvo_feature_pyramid_insert(const void* src, void* const* dst, const int* scale, int L, int C,
                                 int H, int W, int dtype, void* stream);
+/* Ring variant of dpvo_feature_pyramid_insert for graph-replayed frames: dst0[l]
+   is slot 0 of level l's ring, slots slot_bytes[l] apart; the slot written is
+   *slot_dev % mem, read on the device (replaces the host slot of dpvo.py's
+   fmap1_/fmap2_ ring writes). */
+int dpvo_feature_pyramid_insert_ring(const void* src, void* const* dst0, const int64_t* slot_bytes,
+                                     const int* scale, int L, int C, int H, int W, int mem,
+                                     const int32_t* slot_dev, int dtype, void* stream);
 
 /* A-CORR-BWD.  Replaces cuda_corr.backward (correlation.cpp:58,
    correlation_kernel.cu:275-325 + corr_backward_kernel :178-229).
@@ -326,6 +333,21 @@ int dpvo_reproject_ordered_plan(const float* poses, const float* patches,
                                 const int64_t* kk, int E, int P, int num_poses, int num_patches,
                                 int N2, float* coords, int32_t* order, int t0, int t1,
                                 void* workspace, size_t workspace_bytes, void* stream);
+/* Device-scalar variants for graph-replayed DPVO updates (the window start t0
+   moves every frame, shapes stay fixed): t0 is read from the int32 device
+   scalar *t0_dev, N = t1 - t0 is given.  Same results as the host-t0 calls. */
+int dpvo_reproject_ordered_plan_dev(const float* poses, const float* patches,
+                                    const float* intrinsics, const int64_t* ii, const int64_t* jj,
+                                    const int64_t* kk, int E, int P, int num_poses,
+                                    int num_patches, int N2, float* coords, int32_t* order,
+                                    const int32_t* t0_dev, int N, void* workspace,
+                                    size_t workspace_bytes, void* stream);
+int dpvo_ba_forward_planned_dev(float* poses, float* patches, const float* intrinsics,
+                                const float* target, const float* weight, const float* lmbda,
+                                const int64_t* ii, const int64_t* jj, const int64_t* kk, int E,
+                                int P, int num_poses, int num_patches, const int32_t* t0_dev,
+                                int N, int iterations, void* workspace, size_t workspace_bytes,
+                                void* stream);
 
 /* F-NBR.  Replaces cuda_ba.neighbors (ba.cpp:59-97).  Groups edges by ii,
    stable-sorts each group by jj; ix = previous edge, jx = next edge, -1 at
@@ -385,6 +407,16 @@ int dpvo_pg_remove(const uint8_t* mask, const int64_t* ix, int64_t thresh, int64
                    float* weight_b, float* target_b, int64_t* ii_i, int64_t* jj_i, int64_t* kk_i,
                    float* weight_i, float* target_i, int DIM, int* counts, int* pos,
                    int max_edges, void* stream);
+/* DPVO.keyframe's window removal (dpvo.py:684-693) with thresholds relative to
+   the device frame count n = *n_dev: remove ix[kk] < n + thresh_off, except
+   (lc_on) edges with jj - ii > 30 and jj > n + lc_off.  Graph-replayable. */
+int dpvo_pg_remove_window_dev(const int64_t* ix, const int32_t* n_dev, int64_t thresh_off,
+                              int64_t lc_off, int lc_on, int store, int64_t* ii, int64_t* jj,
+                              int64_t* kk, float* net, float* weight, float* target,
+                              int64_t* ii_b, int64_t* jj_b, int64_t* kk_b, float* net_b,
+                              float* weight_b, float* target_b, int64_t* ii_i, int64_t* jj_i,
+                              int64_t* kk_i, float* weight_i, float* target_i, int DIM,
+                              int* counts, int* pos, int max_edges, void* stream);
 
 #ifdef __cplusplus
 }

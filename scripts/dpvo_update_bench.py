@@ -1,8 +1,10 @@
 """Per-frame timing of DPVO's update data flow on the MI355X ops
-(dpvo_amd/update.py: insertion, device patch graph, reproject, corr levels
-[1,4], synthetic oracle network, fastba.BA window, keyframe-window removal).
+(dpvo_amd/update.py: insertion, device patch graph, reproject + plan, corr
+levels [1,4], deterministic oracle network, fastba.BA window, keyframe-window
+removal), eager and as replayed hipGraphs, plus the window pose error before
+and after a global scale (monocular BA fixes the scene only up to scale).
 
-    python scripts/dpvo_update_bench.py [frames=60] [M=96] [ba_iters=2] [fp16]
+    python scripts/dpvo_update_bench.py [frames=80] [M=20] [ba_iters=1]
 """
 import json
 import os
@@ -11,23 +13,26 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import torch  # noqa: E402
 
-from dpvo_amd import fastba  # noqa: E402
 from dpvo_amd.update import UpdateHarness  # noqa: E402
 
-frames = int(sys.argv[1]) if len(sys.argv) > 1 else 60
-M = int(sys.argv[2]) if len(sys.argv) > 2 else 96
-iters = int(sys.argv[3]) if len(sys.argv) > 3 else 2
-dt = torch.float16 if (len(sys.argv) > 4 and sys.argv[4] == "fp16") else torch.float32
-h = UpdateHarness(M=M, ba_iters=iters, feat_dtype=dt)
-for f in range(frames):
+frames = int(sys.argv[1]) if len(sys.argv) > 1 else 80
+M = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+iters = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+h = UpdateHarness(M=M, ba_iters=iters, buffer=frames + 8)
+warm = 40
+for f in range(warm):
     st = h.step()
-    if f % 10 == 0 or f == frames - 1:
-        print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in st.items()}),
-              flush=True)
-tail = h.stats[frames // 2:]
-keys = [k for k in tail[0] if k.endswith("_ms")]
-med = {k: sorted(s[k] for s in tail)[len(tail) // 2] for k in keys}
-print(json.dumps({"summary": f"median of the last {len(tail)} frames", "M": M, "ba_iters": iters,
-                  "features": str(dt), "edges": tail[-1]["edges"], **med,
-                  "pose_err_m": h.pose_error(),
-                  "ba_status": fastba.cuda_ba.check_status(h.poses)}), flush=True)
+eager = [s["total_ms"] for s in h.stats[-10:]]
+h.capture()
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+ev[0].record()
+h.replay(frames - warm)
+ev[1].record()
+torch.cuda.synchronize()
+per = ev[0].elapsed_time(ev[1]) / (frames - warm)
+err, scale = h.pose_error_scaled()
+print(json.dumps({"M": M, "edges": st["edges"], "ba_iters": iters, "frames": frames,
+                  "eager_ms_per_frame_median": sorted(eager)[len(eager) // 2],
+                  "graph_ms_per_frame": per, "pose_err_m": h.pose_error(),
+                  "pose_err_scaled_m": err, "scale": scale,
+                  "depth_err": h.depth_error(h.n - 20, h.n - 12), "status": h.check()}))

@@ -1,36 +1,126 @@
-"""DPVO.update() data flow on the HIP ops (dpvo_amd/update.py): runs frames
-through insertion, device patch-graph bookkeeping, reproject, corr, the
-synthetic oracle network, fastba.BA on the optimisation window and keyframe
-removal.  Checks the steady-state edge count against DPVO's edge rule, the
-BA status, and that the sliding-window BA recovers the scene: inverse depths
-initialised to 0.6 converge to the truth once observed, poses stay within
-odometry drift of the known trajectory."""
+"""DPVO.update() data flow on the HIP ops (dpvo_amd/update.py), SURVEY 8(f1):
+insertion, device patch-graph bookkeeping, reproject (+ order + BA plan),
+corr levels [1, 4], the deterministic oracle network, fastba.BA on the
+optimisation window (iterations=1, the fork's local call dpvo.py:824) and
+keyframe-window removal, with MAX_EDGES = 10000 (dpvo/config.py:42).
+
+* the eager loop converges and keeps DPVO's steady-state edge count;
+* one frame's corr and BA match the oracle (oracle.corr_fwd, oracle.ba) on
+  the harness's own inputs (tolerances of tests/test_corr_gpu.py and
+  tests/test_ba_gpu.py);
+* the captured update graphs replayed frame after frame give the same bits
+  as the eager loop (device frame scalars, no host sync inside a frame)."""
+import numpy as np
 import pytest
+import torch
+
+import oracle
 
 pytestmark = pytest.mark.gpu
 
 
-def test_update_loop_runs_and_converges(gpu):
-    from dpvo_amd import fastba
-    from dpvo_amd.update import UpdateHarness
-
-    M, r, rw = 8, 13, 22
-    h = UpdateHarness(device=gpu, M=M, lifetime=r, removal_window=rw, max_edges=8000,
-                      buffer=128, pose_noise=0.0, depth_init=0.6)
-    for f in range(40):
-        st = h.step()
-    # steady state: patches of frames >= n - rw keep their edges; each patch of
-    # frame g has edges to frames g-r+1 .. min(g+r-1, n-1) (dpvo.py:838-903)
-    n = h.n
-    expect = 0
+def _expect_edges(n, M, r=13, rw=22):
+    """active edges after the removal of frame n (DPVO's n, dpvo.py:684-693)."""
+    tot = 0
     for g in range(max(n - rw, 0), n):
         lo, hi = max(g - r + 1, 0), min(g + r - 1, n - 1)
-        expect += M * (hi - lo + 1)
-    assert h.pg.num_edges == expect
-    assert fastba.cuda_ba.check_status(h.poses) == 0
+        tot += M * (hi - lo + 1)
+    return tot
+
+
+def test_update_loop_runs_and_converges(gpu):
+    from dpvo_amd.update import UpdateHarness
+
+    M = 8
+    h = UpdateHarness(device=gpu, M=M, buffer=128, pose_noise=0.0, depth_init=0.6)
+    for f in range(40):
+        st = h.step()
+    n = h.n
+    assert h.pg.num_edges == _expect_edges(n, M)
+    assert h.check() == 0
     assert st["corr_shape"] == (1, st["edges"], 7 * 7 * 9 * 2)
     # depths of patches observed in many windows: far closer to the truth than
     # the 0.6 initialisation (whose mean error is ~0.2)
     init = float((h.gt_d[:n * M] - 0.6).abs().mean())
     assert h.depth_error(n - 20, n - 12) < 0.25 * init, (h.depth_error(n - 20, n - 12), init)
     assert h.pose_error() < 0.05
+
+
+def test_max_edges_is_the_reference_cap(gpu):
+    """M = 20 fits MAX_EDGES = 10000 (497 M = 9940 active edges at the BA);
+    M = 21 does not and raises before touching the graph, as the reference's
+    append_factors does (dpvo.py:502-507)."""
+    from dpvo_amd.update import UpdateHarness
+
+    h = UpdateHarness(device=gpu, M=20, buffer=64)
+    for _ in range(40):
+        st = h.step()
+    assert st["edges"] == 9940 and h.pg.max_edges == 10000
+    assert h.check() == 0
+    h = UpdateHarness(device=gpu, M=21, buffer=64)
+    with pytest.raises(RuntimeError, match="MAX_EDGES"):
+        for _ in range(40):
+            h.step()
+
+
+def test_harness_frame_matches_oracle(gpu):
+    """One steady-state frame: corr at both levels vs oracle.corr_fwd on the
+    frame's own coords, and the BA vs oracle.ba on the frame's own inputs."""
+    from dpvo_amd.update import UpdateHarness
+
+    M = 10
+    h = UpdateHarness(device=gpu, M=M, buffer=64)
+    for _ in range(25):
+        h.step()
+    h.keep_inputs = True
+    n = h.n
+    h.step()
+    I = h.last_inputs
+    E = I["ii"].numel()
+    coords = h.last["coords"].cpu().numpy()
+    corr = h.last["corr"].view(1, E, 7, 7, 3, 3, 2).cpu().numpy()
+    kk, jj = I["kk"].cpu().numpy(), I["jj"].cpu().numpy()
+    gm = I["gmap"].cpu().numpy()
+    for lvl, s in enumerate(h.levels):
+        ref = oracle.corr_fwd(gm, I["pyr"][lvl].cpu().numpy(), coords / s, kk % (M * h.pmem),
+                              jj % h.mem, 3)
+        got = corr[..., lvl]
+        assert np.abs(got - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max())
+    t1 = n + 1
+    t0 = t1 - I["N"]
+    Pr, Kr = oracle.ba(I["poses"].cpu().numpy(), I["patches"].cpu().numpy(),
+                       h.intrinsics.cpu().numpy(), I["target"].cpu().numpy(),
+                       I["weight"].cpu().numpy(), 1e-4, I["ii"].cpu().numpy(), jj, kk, t0, t1,
+                       h.ba_iters)
+    P, K = h.poses.cpu().numpy(), h.patches.cpu().numpy()
+    np.testing.assert_allclose(P, Pr, rtol=0, atol=2e-5)
+    np.testing.assert_allclose(K[:, 2], Kr[:, 2], rtol=1e-4, atol=1e-5)
+    assert h.check() == 0
+
+
+def test_graph_replay_matches_eager(gpu):
+    """The update captured as hipGraphs (one per ping-pong parity of the
+    patch-graph buffers) and replayed for 12 frames gives the same bits as 12
+    eager frames: poses, inverse depths, the active edge list and counts."""
+    from dpvo_amd.update import UpdateHarness
+
+    M, warm, frames = 10, 36, 12
+    a = UpdateHarness(device=gpu, M=M, buffer=64)
+    b = UpdateHarness(device=gpu, M=M, buffer=64)
+    for _ in range(warm + frames):
+        a.step()
+    for _ in range(warm):
+        b.step()
+    assert b.steady()
+    b.capture()
+    b.replay(frames)
+    torch.cuda.synchronize()
+    assert a.n == b.n
+    assert torch.equal(a.poses, b.poses)
+    assert torch.equal(a.patches, b.patches)
+    assert torch.equal(a.fs, b.fs)
+    E = a.pg.num_edges
+    assert E == b.pg.num_edges == _expect_edges(a.n, M)
+    for k in ("ii", "jj", "kk"):
+        assert torch.equal(getattr(a.pg, k)[:E], getattr(b.pg, k)[:E]), k
+    assert a.check() == 0 and b.check() == 0
