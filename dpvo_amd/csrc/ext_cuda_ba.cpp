@@ -744,6 +744,137 @@ void pg_remove_window_dev(torch::Tensor ix, torch::Tensor n_dev, int64_t thresh_
                "cuda_ba.pg_remove_window_dev");
 }
 
+void pg_append_dev(torch::Tensor ix, torch::Tensor kk_new, torch::Tensor jj_new,
+                   torch::Tensor n_dev, torch::Tensor ii, torch::Tensor jj, torch::Tensor kk,
+                   torch::Tensor net, torch::Tensor counts) {
+  ix = idx64(ix, "ix");
+  kk_new = idx64(kk_new, "kk");
+  jj_new = idx64(jj_new, "jj");
+  TORCH_CHECK(kk_new.numel() == jj_new.numel(), "kk / jj sizes differ");
+  TORCH_CHECK(ii.is_contiguous() && jj.is_contiguous() && kk.is_contiguous() &&
+              counts.is_contiguous() && counts.scalar_type() == torch::kInt32,
+              "pg buffers must be contiguous, counts int32");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ii.device());
+  const int max_edges = ii.numel();
+  const int DIM = net.defined() && net.numel() ? (int)(net.numel() / max_edges) : 0;
+  check_status(dpvo_pg_append_dev(ix.data_ptr<int64_t>(), kk_new.data_ptr<int64_t>(),
+                                  jj_new.data_ptr<int64_t>(), dev_scalar(n_dev, "n_dev"),
+                                  (int)kk_new.numel(), ii.data_ptr<int64_t>(),
+                                  jj.data_ptr<int64_t>(), kk.data_ptr<int64_t>(), opt_f32(net),
+                                  DIM, counts.data_ptr<int>(), max_edges, current_stream()),
+               "cuda_ba.pg_append_dev");
+}
+
+void pg_remove_frame_dev(torch::Tensor kf, std::vector<torch::Tensor> act,
+                         std::vector<torch::Tensor> back, torch::Tensor counts, torch::Tensor pos) {
+  TORCH_CHECK(act.size() == 6 && back.size() == 6, "act/back: [ii, jj, kk, net, weight, target]");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(counts.device());
+  const int max_edges = act[0].numel();
+  const int DIM = act[3].defined() && act[3].numel() ? (int)(act[3].numel() / max_edges) : 0;
+  auto L = [](const torch::Tensor& t) { return t.data_ptr<int64_t>(); };
+  check_status(dpvo_pg_remove_frame_dev(
+                   dev_scalar(kf, "kf"), L(act[0]), L(act[1]), L(act[2]), opt_f32(act[3]),
+                   act[4].data_ptr<float>(), act[5].data_ptr<float>(), L(back[0]), L(back[1]),
+                   L(back[2]), opt_f32(back[3]), back[4].data_ptr<float>(),
+                   back[5].data_ptr<float>(), DIM, counts.data_ptr<int>(), pos.data_ptr<int>(),
+                   max_edges, current_stream()),
+               "cuda_ba.pg_remove_frame_dev");
+}
+
+// DPVO.keyframe decision (dpvo.py:586-624): kf = {drop, k}, mag = both motionmags
+void kf_motion(torch::Tensor ii, torch::Tensor jj, torch::Tensor kk, torch::Tensor counts,
+               torch::Tensor poses, torch::Tensor patches, torch::Tensor intrinsics,
+               torch::Tensor st, int64_t keyframe_index, double keyframe_thresh, torch::Tensor kf,
+               torch::Tensor mag) {
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  TORCH_CHECK(poses.scalar_type() == torch::kFloat32 && patches.scalar_type() == torch::kFloat32 &&
+                  intrinsics.scalar_type() == torch::kFloat32 && poses.is_contiguous() &&
+                  patches.is_contiguous() && intrinsics.is_contiguous(),
+              "poses / patches / intrinsics: contiguous float32");
+  TORCH_CHECK(mag.scalar_type() == torch::kFloat32 && mag.numel() >= 2 && kf.numel() >= 2,
+              "kf int32[2], mag float32[2]");
+  auto L = [](const torch::Tensor& t) { return t.data_ptr<int64_t>(); };
+  check_status(dpvo_kf_motion(L(idx64(ii, "ii")), L(idx64(jj, "jj")), L(idx64(kk, "kk")),
+                              dev_scalar(counts, "counts"), poses.data_ptr<float>(),
+                              patches.data_ptr<float>(), intrinsics.data_ptr<float>(),
+                              (int)patches.size(-1), dev_scalar(st, "st"), (int)keyframe_index,
+                              keyframe_thresh, const_cast<int32_t*>(dev_scalar(kf, "kf")),
+                              mag.data_ptr<float>(), current_stream()),
+               "cuda_ba.kf_motion");
+}
+
+// the rest of the frame drop (dpvo.py:626-673); frames: per-frame arrays whose
+// leading dim is the frame (ring 0) or a ring slot (ring > 0)
+void kf_shift(torch::Tensor kf, int64_t M, torch::Tensor st, torch::Tensor ii, torch::Tensor jj,
+              torch::Tensor kk, torch::Tensor counts, std::vector<torch::Tensor> frames,
+              std::vector<int64_t> rings, c10::optional<torch::Tensor> poses,
+              c10::optional<torch::Tensor> tstamps, c10::optional<torch::Tensor> delta_log,
+              c10::optional<torch::Tensor> delta_tstamps, c10::optional<torch::Tensor> delta_count) {
+  TORCH_CHECK(frames.size() == rings.size(), "one ring size per frame array");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(counts.device());
+  std::vector<void*> ptrs;
+  std::vector<int64_t> bytes;
+  std::vector<int32_t> ring;
+  for (size_t a = 0; a < frames.size(); a++) {
+    check_device(frames[a], "frame array");
+    TORCH_CHECK(frames[a].is_contiguous() && frames[a].dim() >= 1, "frame arrays contiguous");
+    ptrs.push_back(frames[a].data_ptr());
+    bytes.push_back(frames[a].numel() / frames[a].size(0) * frames[a].element_size());
+    ring.push_back((int32_t)rings[a]);
+  }
+  auto L = [](const torch::Tensor& t) { return t.data_ptr<int64_t>(); };
+  const bool log = delta_log && delta_log->defined();
+  float* dl = nullptr;
+  int64_t* dt = nullptr;
+  int32_t* dc = nullptr;
+  const float* pp = nullptr;
+  const int64_t* ts = nullptr;
+  int cap = 0;
+  if (log) {
+    TORCH_CHECK(poses && tstamps && delta_tstamps && delta_count, "delta log needs all buffers");
+    dl = delta_log->data_ptr<float>();
+    dt = delta_tstamps->data_ptr<int64_t>();
+    dc = const_cast<int32_t*>(dev_scalar(*delta_count, "delta_count"));
+    pp = poses->data_ptr<float>();
+    ts = tstamps->data_ptr<int64_t>();
+    cap = (int)(delta_log->numel() / 7);
+  }
+  check_status(dpvo_kf_shift(dev_scalar(kf, "kf"), (int)M, const_cast<int32_t*>(dev_scalar(st, "st")),
+                             L(ii), L(jj), L(kk), dev_scalar(counts, "counts"), (int)ii.numel(),
+                             ptrs.data(), bytes.data(), ring.data(), (int)ptrs.size(), pp, ts, dl,
+                             dt, dc, cap, current_stream()),
+               "cuda_ba.kf_shift");
+}
+
+// PatchGraph.edges_loop (patchgraph.py:65-91) gated as dpvo.py:984-988
+void edges_loop(torch::Tensor poses, torch::Tensor patches, torch::Tensor intrinsics,
+                torch::Tensor ix, torch::Tensor st, int64_t n_cap,
+                c10::optional<torch::Tensor> last_global_ba, int64_t removal_window,
+                int64_t max_edge_age, int64_t global_opt_freq, int64_t keyframe_index,
+                double backend_thresh, int64_t max_num_edges, int64_t nms, torch::Tensor work,
+                torch::Tensor out_kk, torch::Tensor out_jj, torch::Tensor out_n) {
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  TORCH_CHECK(work.scalar_type() == torch::kFloat32 &&
+                  work.numel() >= (int64_t)dpvo_edges_loop_work_floats(),
+              "work: float32[edges_loop_work_floats()]");
+  const int M = (int)patches.size(-4);
+  TORCH_CHECK(out_kk.numel() >= max_num_edges * M && out_jj.numel() >= max_num_edges * M,
+              "out_kk / out_jj: max_num_edges x M");
+  int32_t* lb = (last_global_ba && last_global_ba->defined())
+                    ? const_cast<int32_t*>(dev_scalar(*last_global_ba, "last_global_ba"))
+                    : nullptr;
+  check_status(dpvo_edges_loop(poses.data_ptr<float>(), patches.data_ptr<float>(),
+                               intrinsics.data_ptr<float>(), idx64(ix, "ix").data_ptr<int64_t>(),
+                               (int)patches.size(-1), M, dev_scalar(st, "st"), (int)n_cap, lb,
+                               (int)removal_window, (int)max_edge_age, (int)global_opt_freq,
+                               (int)keyframe_index, (float)backend_thresh, (int)max_num_edges,
+                               (int)nms, work.data_ptr<float>(), out_kk.data_ptr<int64_t>(),
+                               out_jj.data_ptr<int64_t>(),
+                               const_cast<int32_t*>(dev_scalar(out_n, "out_n")),
+                               current_stream()),
+               "cuda_ba.edges_loop");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("forward", &ba_forward, "BA forward operator");
   m.def("neighbors", &ba_neighbors, "temporal neighboor indicies");
@@ -780,6 +911,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "forward_planned with t0 read from an int32 device scalar (graph replay)");
   m.def("pg_remove_window_dev", &pg_remove_window_dev,
         "DPVO.keyframe window removal with thresholds relative to a device frame count");
+  m.def("pg_append_dev", &pg_append_dev, "append_factors with a device edge count");
+  m.def("pg_remove_frame_dev", &pg_remove_frame_dev,
+        "DPVO.keyframe frame-drop removal predicated on the device decision kf");
+  m.def("kf_motion", &kf_motion, "DPVO.keyframe motion magnitude + decision (dpvo.py:586-624)");
+  m.def("kf_shift", &kf_shift, "DPVO.keyframe frame drop: delta log, edge / frame shift, counters",
+        py::arg("kf"), py::arg("M"), py::arg("st"), py::arg("ii"), py::arg("jj"), py::arg("kk"),
+        py::arg("counts"), py::arg("frames"), py::arg("rings"), py::arg("poses") = py::none(),
+        py::arg("tstamps") = py::none(), py::arg("delta_log") = py::none(),
+        py::arg("delta_tstamps") = py::none(), py::arg("delta_count") = py::none());
+  m.def("edges_loop", &edges_loop, "PatchGraph.edges_loop (patchgraph.py:65-91), device count");
+  m.def("edges_loop_work_floats", []() { return (int64_t)dpvo_edges_loop_work_floats(); });
   m.def("reproject_ordered", &ba_reproject_ordered,
         "reproject + edge order by target frame (for cuda_corr.forward_levels(order=))");
   m.def("select_path", [](int mode) { check_status(dpvo_ba_select_path(mode), "select_path"); },

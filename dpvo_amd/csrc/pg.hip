@@ -33,9 +33,12 @@ struct PgBufs {
 };
 
 // new edges (kk_new, jj_new) at [num, num + n); ii = ix[kk]; net rows zeroed
+// n_dev (device count, e.g. edges_loop's output): n = min(*n_dev, n)
 __global__ void pg_append_kernel(const int64_t* __restrict__ ix, const int64_t* __restrict__ kk_new,
                                  const int64_t* __restrict__ jj_new, int n, PgBufs b, int DIM,
-                                 const int* __restrict__ counts, int max_edges) {
+                                 const int* __restrict__ counts, int max_edges,
+                                 const int* __restrict__ n_dev) {
+  if (n_dev) n = min(*n_dev, n);
   const int num = counts[0];
   if (num + n > max_edges) return;  // flagged by pg_count_kernel
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -52,7 +55,8 @@ __global__ void pg_append_kernel(const int64_t* __restrict__ ix, const int64_t* 
   }
 }
 
-__global__ void pg_count_kernel(int* counts, int n, int max_edges) {
+__global__ void pg_count_kernel(int* counts, int n, int max_edges, const int* __restrict__ n_dev) {
+  if (n_dev) n = min(*n_dev, n);
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     if (counts[0] + n > max_edges) counts[2] |= 1;
     else counts[0] += n;
@@ -68,7 +72,7 @@ __global__ void pg_count_kernel(int* counts, int n, int max_edges) {
 __global__ void __launch_bounds__(kPgT) pg_plan_remove_kernel(
     const uint8_t* __restrict__ mask, const int64_t* __restrict__ ix, int64_t thresh,
     int64_t lc_min, PgBufs a, int* counts, int* __restrict__ pos, int store, int max_edges,
-    const int* n_dev, int lc_on) {
+    const int* n_dev, int lc_on, const int* kf) {
   if (n_dev) {
     const int64_t n = *n_dev;
     thresh += n;
@@ -84,7 +88,9 @@ __global__ void __launch_bounds__(kPgT) pg_plan_remove_kernel(
     const int e = base + tid;
     int rm = 0;
     if (e < num) {
-      if (mask) {
+      if (kf) {  // DPVO.keyframe frame drop (dpvo.py:638-645): kf = {drop, k}
+        rm = (kf[0] && (a.ii[e] == kf[1] || a.jj[e] == kf[1])) ? 1 : 0;
+      } else if (mask) {
         rm = mask[e] ? 1 : 0;
       } else {
         rm = ix[a.kk[e]] < thresh ? 1 : 0;
@@ -194,9 +200,9 @@ PgBufs bufs(int64_t* ii, int64_t* jj, int64_t* kk, float* net, float* weight, fl
 
 using namespace dpvo;
 
-DPVO_EXPORT int dpvo_pg_append(const int64_t* ix, const int64_t* kk_new, const int64_t* jj_new,
-                               int n, int64_t* ii, int64_t* jj, int64_t* kk, float* net, int DIM,
-                               int* counts, int max_edges, void* stream) {
+static int pg_append_impl(const int64_t* ix, const int64_t* kk_new, const int64_t* jj_new, int n,
+                          int64_t* ii, int64_t* jj, int64_t* kk, float* net, int DIM, int* counts,
+                          int max_edges, void* stream, const int32_t* n_dev) {
   if (n <= 0) return DPVO_OK;
   if (!ix || !kk_new || !jj_new || !ii || !jj || !kk || !counts || max_edges <= 0 ||
       (net && DIM <= 0))
@@ -205,11 +211,29 @@ DPVO_EXPORT int dpvo_pg_append(const int64_t* ix, const int64_t* kk_new, const i
   const int64_t work = net ? (int64_t)n * DIM : n;
   const int grid = (int)std::min<int64_t>((work + 255) / 256, 2048);
   hipLaunchKernelGGL(pg_append_kernel, dim3(grid < 1 ? 1 : grid), dim3(256), 0, st, ix, kk_new,
-                     jj_new, n, bufs(ii, jj, kk, net, nullptr, nullptr), DIM, counts, max_edges);
+                     jj_new, n, bufs(ii, jj, kk, net, nullptr, nullptr), DIM, counts, max_edges,
+                     (const int*)n_dev);
   int rc = launch_status();
   if (rc) return rc;
-  hipLaunchKernelGGL(pg_count_kernel, dim3(1), dim3(64), 0, st, counts, n, max_edges);
+  hipLaunchKernelGGL(pg_count_kernel, dim3(1), dim3(64), 0, st, counts, n, max_edges,
+                     (const int*)n_dev);
   return launch_status();
+}
+
+DPVO_EXPORT int dpvo_pg_append(const int64_t* ix, const int64_t* kk_new, const int64_t* jj_new,
+                               int n, int64_t* ii, int64_t* jj, int64_t* kk, float* net, int DIM,
+                               int* counts, int max_edges, void* stream) {
+  return pg_append_impl(ix, kk_new, jj_new, n, ii, jj, kk, net, DIM, counts, max_edges, stream,
+                        nullptr);
+}
+
+DPVO_EXPORT int dpvo_pg_append_dev(const int64_t* ix, const int64_t* kk_new, const int64_t* jj_new,
+                                   const int32_t* n_dev, int n_cap, int64_t* ii, int64_t* jj,
+                                   int64_t* kk, float* net, int DIM, int* counts, int max_edges,
+                                   void* stream) {
+  if (!n_dev) return DPVO_ERR_INVALID;
+  return pg_append_impl(ix, kk_new, jj_new, n_cap, ii, jj, kk, net, DIM, counts, max_edges,
+                        stream, n_dev);
 }
 
 static int pg_remove_impl(const uint8_t* mask, const int64_t* ix, int64_t thresh, int64_t lc_min,
@@ -218,9 +242,10 @@ static int pg_remove_impl(const uint8_t* mask, const int64_t* ix, int64_t thresh
                           int64_t* kk_b, float* net_b, float* weight_b, float* target_b,
                           int64_t* ii_i, int64_t* jj_i, int64_t* kk_i, float* weight_i,
                           float* target_i, int DIM, int* counts, int* pos, int max_edges,
-                          void* stream, const int32_t* n_dev, int lc_on) {
+                          void* stream, const int32_t* n_dev, int lc_on,
+                          const int32_t* kf = nullptr) {
   if (!ii || !jj || !kk || !weight || !target || !ii_b || !jj_b || !kk_b || !weight_b ||
-      !target_b || !counts || !pos || max_edges <= 0 || (!mask && !ix) || (net && !net_b) ||
+      !target_b || !counts || !pos || max_edges <= 0 || (!mask && !ix && !kf) || (net && !net_b) ||
       (net && (DIM <= 0 || DIM % 4)) || (store && (!ii_i || !jj_i || !kk_i || !weight_i || !target_i)))
     return DPVO_ERR_INVALID;
   hipStream_t st = as_stream(stream);
@@ -228,7 +253,8 @@ static int pg_remove_impl(const uint8_t* mask, const int64_t* ix, int64_t thresh
   const PgBufs b = bufs(ii_b, jj_b, kk_b, net_b, weight_b, target_b);
   const PgBufs in = bufs(ii_i, jj_i, kk_i, nullptr, weight_i, target_i);
   hipLaunchKernelGGL(pg_plan_remove_kernel, dim3(1), dim3(kPgT), 0, st, mask, ix, thresh, lc_min,
-                     a, counts, pos, store, max_edges, (const int*)n_dev, lc_on);
+                     a, counts, pos, store, max_edges, (const int*)n_dev, lc_on,
+                     (const int*)kf);
   int rc = launch_status();
   if (rc) return rc;
   const int64_t work = net ? (int64_t)max_edges * (DIM / 4) : max_edges;
@@ -265,4 +291,15 @@ DPVO_EXPORT int dpvo_pg_remove_window_dev(const int64_t* ix, const int32_t* n_de
   return pg_remove_impl(nullptr, ix, thresh_off, lc_off, store, ii, jj, kk, net, weight, target,
                         ii_b, jj_b, kk_b, net_b, weight_b, target_b, ii_i, jj_i, kk_i, weight_i,
                         target_i, DIM, counts, pos, max_edges, stream, n_dev, lc_on);
+}
+
+DPVO_EXPORT int dpvo_pg_remove_frame_dev(const int32_t* kf, int64_t* ii, int64_t* jj, int64_t* kk,
+                                         float* net, float* weight, float* target, int64_t* ii_b,
+                                         int64_t* jj_b, int64_t* kk_b, float* net_b,
+                                         float* weight_b, float* target_b, int DIM, int* counts,
+                                         int* pos, int max_edges, void* stream) {
+  if (!kf) return DPVO_ERR_INVALID;
+  return pg_remove_impl(nullptr, nullptr, 0, -1, 0, ii, jj, kk, net, weight, target, ii_b, jj_b,
+                        kk_b, net_b, weight_b, target_b, nullptr, nullptr, nullptr, nullptr,
+                        nullptr, DIM, counts, pos, max_edges, stream, nullptr, 0, kf);
 }

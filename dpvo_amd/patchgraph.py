@@ -114,5 +114,71 @@ class DevicePatchGraph:
                                         self.target_inac], self.counts, self._pos)
         self._a, self._b = b, a
 
+    def append_factors_dev(self, ix, kk, jj, n_dev):
+        """append_factors of the first min(n_dev, len(kk)) edges, n_dev an
+        int32 device scalar (edges_loop's count, dpvo.py:986-988)."""
+        a = self._a
+        self._ext.pg_append_dev(ix, kk.contiguous(), jj.contiguous(), n_dev, a["ii"], a["jj"],
+                                a["kk"], a["net"], self.counts)
+
+    def keyframe(self, st, poses, patches, intrinsics, M, frames=(), rings=(), tstamps=None,
+                 keyframe_index=4, keyframe_thresh=12.5, kf=None, mag=None, delta=None):
+        """DPVO.keyframe's frame drop (dpvo.py:586-673) on the device, no host
+        sync: the decision (motionmag of frames n-KI-1 <-> n-KI+1 below
+        KEYFRAME_THRESH) is a device flag kf = {drop, k} that predicates the
+        removal of the edges touching k (not stored), the edge index shift,
+        the move of every per-frame array in `frames` (ring[a] > 0: row =
+        frame % ring) and n -= 1, m -= M in st = {n, m} (int32 device).
+        poses / patches / intrinsics / tstamps are the per-frame buffers
+        (patches [N*M,3,P,P]); they are shifted too.  delta = (log [cap,7],
+        tstamps [cap,2] (t1, t0), count int32[1]) records pg.delta.
+        Returns (kf, mag) device tensors."""
+        dev = self.counts.device
+        kf = torch.zeros(2, dtype=torch.int32, device=dev) if kf is None else kf
+        mag = torch.zeros(2, dtype=torch.float32, device=dev) if mag is None else mag
+        a, b = self._a, self._b
+        self._ext.kf_motion(a["ii"], a["jj"], a["kk"], self.counts, poses, patches, intrinsics,
+                            st, int(keyframe_index), float(keyframe_thresh), kf, mag)
+        keys = ("ii", "jj", "kk", "net", "weight", "target")
+        self._ext.pg_remove_frame_dev(kf, [a[k] for k in keys], [b[k] for k in keys],
+                                      self.counts, self._pos)
+        self._a, self._b = b, a
+        a = self._a
+        # per-frame rows: patches [N*M, 3, P, P] moves M patches per frame
+        fr = [poses, patches.view(patches.shape[0] // M, -1), intrinsics] + ([tstamps] if tstamps is not None else []) + list(frames)
+        rg = [0, 0, 0] + ([0] if tstamps is not None else []) + [int(r) for r in rings]
+        if len(frames) != len(rings):
+            raise ValueError("one ring size per frame array")
+        dl = dt = dc = None
+        if delta is not None:
+            if tstamps is None:
+                raise ValueError("the delta log needs tstamps")
+            dl, dt, dc = delta
+        self._ext.kf_shift(kf, int(M), st, a["ii"], a["jj"], a["kk"], self.counts, fr, rg,
+                           poses if dl is not None else None, tstamps if dl is not None else None,
+                           dl, dt, dc)
+        return kf, mag
+
+    def edges_loop(self, poses, patches, intrinsics, ix, st, n_cap, M, last_global_ba=None,
+                   removal_window=20, max_edge_age=1000, global_opt_freq=15, keyframe_index=4,
+                   backend_thresh=64.0, max_num_edges=1000, nms=1, out=None):
+        """PatchGraph.edges_loop (patchgraph.py:65-91) on the device for the
+        frame count st[0] (n_cap >= n sizes the launch); with last_global_ba
+        (int32 device scalar) gated and updated as dpvo.py:984-988.
+        Returns (kk, jj, count) -- count an int32 device scalar (edges x M);
+        append them with append_factors_dev(ix, kk, jj, count)."""
+        dev = self.counts.device
+        if out is None:
+            out = (torch.empty(max_num_edges * M, dtype=torch.long, device=dev),
+                   torch.empty(max_num_edges * M, dtype=torch.long, device=dev),
+                   torch.zeros(1, dtype=torch.int32, device=dev),
+                   torch.empty(self._ext.edges_loop_work_floats(), device=dev))
+        kk, jj, cnt, work = out
+        self._ext.edges_loop(poses, patches, intrinsics, ix, st, int(n_cap), last_global_ba,
+                             int(removal_window), int(max_edge_age), int(global_opt_freq),
+                             int(keyframe_index), float(backend_thresh), int(max_num_edges),
+                             int(nms), work, kk, jj, cnt)
+        return kk, jj, cnt
+
 
 __all__ = ["DevicePatchGraph"]

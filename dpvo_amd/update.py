@@ -15,14 +15,25 @@ OPTIMIZATION_WINDOW 10; mem = pmem = 36; MAX_EDGES 10000, dpvo/config.py:42):
                     -> fastba.BA(t0 = n - OPTIMIZATION_WINDOW, t1 = n, iterations=1)
                     (dpvo.py:818-824: the fork's local call, python_ba_wrapper with
                     iterations=1, here on the HIP fastba)
-  keyframe removal  edges of patches older than n - REMOVAL_WINDOW moved to the
-                    inactive store (dpvo.py:684-693)
+  keyframe()        (keyframes=True) the frame drop of dpvo.py:601-673 on the device
+                    (DevicePatchGraph.keyframe: motion magnitude, decision flag,
+                    edge removal + index shift, every per-frame buffer and ring
+                    shifted, n -= 1), then the window removal: edges of patches
+                    older than n - REMOVAL_WINDOW moved to the inactive store
+                    (dpvo.py:684-693)
 
 Every per-frame scalar the kernels need (frame count n, ring slots, the BA
 window start t0) lives in a small int32 device tensor (`fs`), so once the
 edge count is steady (it is, with the window rule) ONE update is captured as
 a hipGraph (`capture()`) and replayed for every later frame (`replay()`): no
 host synchronisation and no per-kernel launch from Python inside a frame.
+With keyframes=True the edge count depends on which frames were dropped, so
+the harness reads n and the edge count back once per frame, as the
+reference does (its num_edges / n are host integers): eager only.
+
+Frames are inserted by timestamp t (the synthetic truth, the initial pose and
+patches and the features are functions of t) at buffer index n; with frame
+drops t and n part, and the truth moves with the frame data.
 
 The update network (net.py) needs trained weights that are absent, so a
 deterministic "oracle network" stands in: delta = (true reprojection - coords)
@@ -50,13 +61,16 @@ from .synthetic import channels_last, se3_exp
 class UpdateHarness:
     def __init__(self, device="cuda", M=20, lifetime=13, removal_window=22, opt_window=10,
                  mem=36, H=120, W=160, C=128, DIM=384, max_edges=10000, buffer=512,
-                 ba_iters=1, seed=0, feat_dtype=torch.float32, pose_noise=0.01, depth_init=0.6):
+                 ba_iters=1, seed=0, feat_dtype=torch.float32, pose_noise=0.01, depth_init=0.6,
+                 keyframes=False, keyframe_index=4, keyframe_thresh=12.5):
         self.dev = torch.device(device)
         self.M, self.r, self.rw, self.ow = M, lifetime, removal_window, opt_window
         self.mem = self.pmem = mem
         self.H, self.W, self.C = H, W, C
         self.ba_iters = ba_iters
+        self.keyframes, self.ki, self.kthresh = keyframes, keyframe_index, keyframe_thresh
         self.n = 0
+        self.t = 0
         g = torch.Generator().manual_seed(seed)
         N = buffer
         self.buffer = N
@@ -66,23 +80,29 @@ class UpdateHarness:
         xi[:, 2] = 0.04 * t
         xi[:, 0] = 0.05 * torch.sin(0.1 * t)
         xi[:, 4] = 0.02 * torch.sin(0.07 * t)
-        self.gt_poses = torch.from_numpy(se3_exp(xi.numpy())).float().to(self.dev)
-        self.poses = self.gt_poses.clone()
-        self.poses[:, :3] += pose_noise * torch.randn(N, 3, generator=g).to(self.dev)
-        self.poses[0] = self.gt_poses[0]
+        # by timestamp: truth and initial values (copied to index n on insertion)
+        self.gt_poses_t = torch.from_numpy(se3_exp(xi.numpy())).float().to(self.dev)
+        self.init_poses_t = self.gt_poses_t.clone()
+        self.init_poses_t[:, :3] += pose_noise * torch.randn(N, 3, generator=g).to(self.dev)
+        self.init_poses_t[0] = self.gt_poses_t[0]
+        self.gt_poses = self.gt_poses_t.clone()
+        self.poses = self.init_poses_t.clone()
         P = 3
         self.P = P
         cxy = torch.stack([torch.rand(N * M, generator=g) * (W - 9) + 4,
                            torch.rand(N * M, generator=g) * (H - 9) + 4], -1).floor()
-        self.gt_d = (torch.rand(N * M, generator=g) * 0.8 + 0.3).to(self.dev)
+        gt_d = (torch.rand(N * M, generator=g) * 0.8 + 0.3).to(self.dev)
         off = torch.arange(P, dtype=torch.float32) - P // 2
         patches = torch.zeros(N * M, 3, P, P)
         patches[:, 0] = cxy[:, 0].view(-1, 1, 1) + off.view(1, 1, P)
         patches[:, 1] = cxy[:, 1].view(-1, 1, 1) + off.view(1, P, 1)
         patches[:, 2] = depth_init  # DPVO initialises new patch depths to a median
-        self.patches = patches.to(self.dev)
-        self.gt_patches = self.patches.clone()
-        self.gt_patches[:, 2] = self.gt_d.view(-1, 1, 1)
+        self.init_patches_t = patches.to(self.dev)
+        self.gt_patches_t = self.init_patches_t.clone()
+        self.gt_patches_t[:, 2] = gt_d.view(-1, 1, 1)
+        self.patches = self.init_patches_t.clone()
+        self.gt_patches = self.gt_patches_t.clone()
+        self.tstamps = torch.arange(N, dtype=torch.long, device=self.dev)
         self.intrinsics = torch.tensor([80.0, 80.0, 80.0, 60.0]).view(1, 4).repeat(N, 1).to(self.dev)
         self.ix = torch.arange(N, device=self.dev).repeat_interleave(M)
         # feature rings: channels-last pyramid (levels 1, 4) and gmap
@@ -95,8 +115,16 @@ class UpdateHarness:
         self.lmbda = torch.tensor([1e-4], device=self.dev)
         self.feat_dtype = feat_dtype
         # device frame state: [0] n (frames before this step), [1] t0 of the BA
-        # window, [2] n + 1 (DPVO's n after the increment), [3] n % pmem
+        # window, [2] n + 1 (DPVO's n after the increment), [3] DPVO's m
+        # ([2:4] is keyframe()'s {n, m}), [4] n % pmem, [5] timestamp t
         self.fs = torch.zeros(8, dtype=torch.int32, device=self.dev)
+        if keyframes:
+            self._kf = (torch.zeros(2, dtype=torch.int32, device=self.dev),
+                        torch.zeros(2, dtype=torch.float32, device=self.dev))
+            self.delta = (torch.zeros(N, 7, device=self.dev),
+                          torch.zeros(N, 2, dtype=torch.long, device=self.dev),
+                          torch.zeros(1, dtype=torch.int32, device=self.dev))
+            self.dropped = 0
         self._arM = torch.arange(M, device=self.dev)
         self.graph = None
         self.keep_inputs = False
@@ -108,17 +136,26 @@ class UpdateHarness:
         fs = self.fs
         fs[2:3].copy_(fs[0:1] + 1)
         fs[1:2].copy_(torch.clamp_min(fs[2:3] - self.ow, 1))
-        fs[3:4].copy_(torch.remainder(fs[0:1], self.pmem))
+        fs[3:4].copy_(fs[2:3] * self.M)
+        fs[4:5].copy_(torch.remainder(fs[0:1], self.pmem))
 
     # -- dpvo.py __call__: features of the new frame ------------------------
     def _insert_frame(self):
-        nf = self.fs[0:1].float()
-        fmap = (0.25 * torch.sin(self.field + 0.37 * nf)).to(self.feat_dtype)
+        tf = self.fs[5:6].float()
+        fmap = (0.25 * torch.sin(self.field + 0.37 * tf)).to(self.feat_dtype)
         altcorr.insert_frame_ring(fmap, self.pyr, self.fs[0:1], self.levels)
-        n64 = self.fs[0:1].long()
+        n64, t64 = self.fs[0:1].long(), self.fs[5:6].long()
+        # the frame's truth / initial values: timestamp row t -> index row n
+        for dst, src in ((self.poses, self.init_poses_t), (self.gt_poses, self.gt_poses_t)):
+            dst.index_copy_(0, n64, src.index_select(0, t64))
+        tidx = t64 * self.M + self._arM
         idx = n64 * self.M + self._arM
+        for dst, src in ((self.patches, self.init_patches_t),
+                         (self.gt_patches, self.gt_patches_t)):
+            dst.index_copy_(0, idx, src.index_select(0, tidx))
+        self.tstamps.index_copy_(0, n64, t64)
         ctr = self.patches.index_select(0, idx)[:, :2, 1, 1].unsqueeze(0)
-        rows = self.fs[3:4].long() * self.M + self._arM
+        rows = self.fs[4:5].long() * self.M + self._arM
         g = altcorr.patchify(fmap.unsqueeze(0), ctr, 1)[0]
         self.gmap[0].index_copy_(0, rows, g)
 
@@ -146,12 +183,16 @@ class UpdateHarness:
         weight = torch.full_like(c, 0.5)
         return delta, weight
 
-    def _update_ops(self, n, E):
-        """Everything of one frame after the host decided the shapes (n, E)."""
+    def _frame_start(self, n):
         self._frame_scalars()
         self._insert_frame()
         kk_new, jj_new = self._edges(n)
         self.pg.append_factors(self.ix, kk_new, jj_new)
+
+    def _update_ops(self, n, E, started=False):
+        """Everything of one frame after the host decided the shapes (n, E)."""
+        if not started:
+            self._frame_start(n)
         ii, jj, kk = self.pg.ii[:E], self.pg.jj[:E], self.pg.kk[:E]
         n1 = n + 1
         N = n1 - max(n1 - self.ow, 1)
@@ -173,9 +214,29 @@ class UpdateHarness:
         fastba.BA_dev(self.poses, self.patches, self.intrinsics, self.pg.target[:, :E],
                       self.pg.weight[:, :E], self.lmbda, ii, jj, kk, t0d, N, ws,
                       iterations=self.ba_iters)
+        if self.keyframes:
+            self._keyframe()
         self.pg.remove_by_window_dev(self.ix, self.fs[2:3], self.rw)
-        self.fs[0:1].add_(1)
+        self.fs[0:1].copy_(self.fs[2:3])
+        self.fs[5:6].add_(1)
         self.last = {"coords": coords, "corr": corr, "ws": ws}
+
+    def _keyframe(self):
+        """dpvo.py:601-673 on the device: every per-frame buffer the harness
+        keeps moves with the dropped frame (rings: the pyramid levels and the
+        gmap by slot; the truth by index)."""
+        M = self.M
+        frames = [self.gt_poses, self.gt_patches.view(self.buffer, -1)]
+        rings = [0, 0]
+        for p in self.pyr:  # channels-last storage [1, mem, H, W, C]
+            frames.append(p.permute(0, 1, 3, 4, 2).reshape(self.mem, -1))
+            rings.append(self.mem)
+        frames.append(self.gmap.view(self.pmem, -1))
+        rings.append(self.pmem)
+        self.pg.keyframe(self.fs[2:4], self.poses, self.patches, self.intrinsics, M,
+                         frames=frames, rings=rings, tstamps=self.tstamps,
+                         keyframe_index=self.ki, keyframe_thresh=self.kthresh,
+                         kf=self._kf[0], mag=self._kf[1], delta=self.delta)
 
     def _edges_after_append(self, n):
         """Host count of active edges after frame n's append: the window rule
@@ -194,17 +255,28 @@ class UpdateHarness:
     def step(self):
         """One frame, eagerly: insertion, edges, update (reproject, corr,
         network, BA), removal.  Returns per-phase host wall-clock ms."""
-        if self.n + 1 >= self.buffer:
+        if self.t + 1 >= self.buffer:  # t >= n (frames dropped)
             raise RuntimeError("UpdateHarness: frame buffer exhausted")
         n = self.n
-        E = self._edges_after_append(n)
-        if E > self.pg.max_edges:
-            raise RuntimeError(f"{E} active edges exceed MAX_EDGES={self.pg.max_edges} "
-                               "(dpvo.py:502-507 raises too)")
         t = time.perf_counter()
-        self._update_ops(n, E)
-        torch.cuda.synchronize()
-        self.n += 1
+        if self.keyframes:  # edge count after the append: read back (host int in DPVO)
+            self._frame_start(n)
+            E = self.pg.num_edges
+            if self.pg.errors & 1:
+                raise RuntimeError(f"active edges exceed MAX_EDGES={self.pg.max_edges} "
+                                   "(dpvo.py:502-507 raises too)")
+            self._update_ops(n, E, started=True)
+            self.n = int(self.fs[0].item())
+            self.dropped += n + 1 - self.n
+        else:
+            E = self._edges_after_append(n)
+            if E > self.pg.max_edges:
+                raise RuntimeError(f"{E} active edges exceed MAX_EDGES={self.pg.max_edges} "
+                                   "(dpvo.py:502-507 raises too)")
+            self._update_ops(n, E)
+            torch.cuda.synchronize()
+            self.n += 1
+        self.t += 1
         st = {"frame": self.n, "edges": E, "corr_shape": tuple(self.last["corr"].shape),
               "total_ms": 1e3 * (time.perf_counter() - t)}
         self.stats.append(st)
@@ -221,6 +293,8 @@ class UpdateHarness:
         The patch-graph removal compacts into the other of two buffer sets
         (ping-pong), so a frame's graph depends on which set is active: two
         graphs are captured, one per parity, and replay() alternates them."""
+        if self.keyframes:
+            raise RuntimeError("capture(): frame drops make the edge count data-dependent")
         if not self.steady():
             raise RuntimeError("capture() needs the steady state (call step() first)")
         n, E = self.n, self._edges_after_append(self.n)
@@ -252,6 +326,7 @@ class UpdateHarness:
             self._parity ^= 1
             self.pg._a, self.pg._b = self.pg._b, self.pg._a  # the set the next frame reads
             self.n += 1
+            self.t += 1
 
     def check(self):
         """Raise on a recorded device-side failure (synchronises): an append
@@ -265,7 +340,7 @@ class UpdateHarness:
     def depth_error(self, lo, hi):
         """Mean |inverse depth - truth| of the patches of frames [lo, hi)."""
         s = slice(lo * self.M, hi * self.M)
-        return float((self.patches[s, 2, 1, 1] - self.gt_d[s]).abs().mean())
+        return float((self.patches[s, 2, 1, 1] - self.gt_patches[s, 2, 1, 1]).abs().mean())
 
     def pose_error(self):
         """Mean translation error of the optimised window vs ground truth (m)."""

@@ -417,6 +417,62 @@ int dpvo_pg_remove_window_dev(const int64_t* ix, const int32_t* n_dev, int64_t t
                               float* weight_b, float* target_b, int64_t* ii_i, int64_t* jj_i,
                               int64_t* kk_i, float* weight_i, float* target_i, int DIM,
                               int* counts, int* pos, int max_edges, void* stream);
+/* append_factors with a device count: n = min(*n_dev, n_cap) edges (e.g. the
+   output of dpvo_edges_loop, dpvo.py:986-988).  Graph-replayable. */
+int dpvo_pg_append_dev(const int64_t* ix, const int64_t* kk_new, const int64_t* jj_new,
+                       const int32_t* n_dev, int n_cap, int64_t* ii, int64_t* jj, int64_t* kk,
+                       float* net, int DIM, int* counts, int max_edges, void* stream);
+/* DPVO.keyframe's frame-drop removal (dpvo.py:633-641): when kf[0] (the
+   device decision of dpvo_kf_motion), remove the active edges with ii == kf[1]
+   or jj == kf[1], not stored.  Always compacts into the *_b buffers (a copy
+   when nothing is dropped), so the caller swaps unconditionally. */
+int dpvo_pg_remove_frame_dev(const int32_t* kf, int64_t* ii, int64_t* jj, int64_t* kk,
+                             float* net, float* weight, float* target, int64_t* ii_b,
+                             int64_t* jj_b, int64_t* kk_b, float* net_b, float* weight_b,
+                             float* target_b, int DIM, int* counts, int* pos, int max_edges,
+                             void* stream);
+
+/* ---------------------------------------------------------------- keyframe */
+
+/* DPVO.keyframe's decision (dpvo.py:586-599, 619-624) on the device.  st =
+   {n, m} (device frame counters), i = n - keyframe_index - 1,
+   j = n - keyframe_index + 1; motionmag over the active edges with
+   projective_ops.flow_mag (projective_ops.py:120-130, beta 0.5).  Writes
+   kf = {drop, k = n - keyframe_index} and mag = {motionmag(i,j),
+   motionmag(j,i)}.  No host synchronisation: kf predicates
+   dpvo_pg_remove_frame_dev and dpvo_kf_shift. */
+int dpvo_kf_motion(const int64_t* ii, const int64_t* jj, const int64_t* kk, const int32_t* counts,
+                   const float* poses, const float* patches, const float* intrinsics, int P,
+                   const int32_t* st, int keyframe_index, double keyframe_thresh, int32_t* kf,
+                   float* mag, void* stream);
+/* The rest of a frame drop (dpvo.py:626-673), predicated on kf[0]: log
+   (t1, t0, poses[k] * poses[k-1]^-1) as pg.delta[t1] into delta_log[7 x cap] /
+   delta_tstamps[2 x cap] at *delta_count (optional: all three null), shift the
+   active edges past k (kk -= M, ii -= 1; jj -= 1), move the per-frame rows
+   k+1 .. n-1 of every frame array one row down (ring[a] > 0: row = frame %
+   ring[a], the imap/gmap/fmap rings), then n -= 1, m -= M. */
+int dpvo_kf_shift(const int32_t* kf, int M, int32_t* st, int64_t* ii, int64_t* jj, int64_t* kk,
+                  const int32_t* counts, int max_edges, void* const* frame_arrays,
+                  const int64_t* bytes_per_frame, const int32_t* ring, int narrays,
+                  const float* poses, const int64_t* tstamps, float* delta_log,
+                  int64_t* delta_tstamps, int32_t* delta_count, int delta_cap, void* stream);
+/* PatchGraph.edges_loop (dpvo/patchgraph.py:65-91, reduce_edges
+   loop_closure/optim_utils.py:24-60) gated like its caller (dpvo.py:984-988:
+   only when n - *last_global_ba >= global_opt_freq; *last_global_ba = n when
+   edges are found; last_global_ba may be null = no gate).  n = st[0] on the
+   device, n_cap >= n sizes the launch.  Writes kk (i M + arange(M)) and jj of
+   the accepted loop edges and their count (edges x M) to out_n, ready for
+   dpvo_pg_append_dev.  work: dpvo_edges_loop_work_floats() floats.
+   Limits: (global_opt_freq - keyframe_index) x min(n_cap - removal_window,
+   max_edge_age) <= 16384, n_cap x (global_opt_freq - keyframe_index) <=
+   131072, max_num_edges <= 1024. */
+int dpvo_edges_loop(const float* poses, const float* patches, const float* intrinsics,
+                    const int64_t* ix, int P, int M, const int32_t* st, int n_cap,
+                    int32_t* last_global_ba, int removal_window, int max_edge_age,
+                    int global_opt_freq, int keyframe_index, float backend_thresh,
+                    int max_num_edges, int nms, float* work, int64_t* out_kk, int64_t* out_jj,
+                    int32_t* out_n, void* stream);
+size_t dpvo_edges_loop_work_floats(void);
 
 #ifdef __cplusplus
 }

@@ -1224,3 +1224,115 @@ ORC_API int orc_lie_bwd(int group, int op, int n, const double* grad, const doub
   }
   return 0;
 }
+
+/* ------------------------------------------------------------------------ */
+/* F-FLOW: projective_ops.flow_mag (projective_ops.py:120-130) over          */
+/* transform (:53-110) with lietorch's fp32 group ops (se3.h inv 325-327,    */
+/* mul 334-336, act4; quaternion renormalised at every load, so3.h:95-97).   */
+/* Op by op in fp32 (-std=c99: no contraction), as the reference's kernels.  */
+/* ------------------------------------------------------------------------ */
+typedef struct { float t[3], q[4]; } g7f;
+
+static g7f g7_load(const float* d) {
+  g7f g;
+  float n;
+  g.t[0] = d[0]; g.t[1] = d[1]; g.t[2] = d[2];
+  n = sqrtf(d[3] * d[3] + d[4] * d[4] + d[5] * d[5] + d[6] * d[6]);
+  g.q[0] = d[3] / n; g.q[1] = d[4] / n; g.q[2] = d[5] / n; g.q[3] = d[6] / n;
+  return g;
+}
+static g7f g7_reload(g7f g) {
+  float d[7] = {g.t[0], g.t[1], g.t[2], g.q[0], g.q[1], g.q[2], g.q[3]};
+  return g7_load(d);
+}
+static void g7_qact(const float* q, const float* p, float* o) { /* so3.h:115-120 */
+  float uv[3], c[3];
+  uv[0] = q[1] * p[2] - q[2] * p[1];
+  uv[1] = q[2] * p[0] - q[0] * p[2];
+  uv[2] = q[0] * p[1] - q[1] * p[0];
+  uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+  c[0] = q[1] * uv[2] - q[2] * uv[1];
+  c[1] = q[2] * uv[0] - q[0] * uv[2];
+  c[2] = q[0] * uv[1] - q[1] * uv[0];
+  for (int i = 0; i < 3; i++) o[i] = p[i] + q[3] * uv[i] + c[i];
+}
+static g7f g7_inv(g7f g) {
+  g7f o;
+  float t[3];
+  const float n = sqrtf(g.q[0] * g.q[0] + g.q[1] * g.q[1] + g.q[2] * g.q[2] + g.q[3] * g.q[3]);
+  o.q[0] = -g.q[0] / n; o.q[1] = -g.q[1] / n; o.q[2] = -g.q[2] / n; o.q[3] = g.q[3] / n;
+  g7_qact(o.q, g.t, t);
+  o.t[0] = -t[0]; o.t[1] = -t[1]; o.t[2] = -t[2];
+  return o;
+}
+static g7f g7_mul(g7f a, g7f b) {
+  g7f o;
+  float t[3];
+  const float x = a.q[3] * b.q[0] + a.q[0] * b.q[3] + a.q[1] * b.q[2] - a.q[2] * b.q[1];
+  const float y = a.q[3] * b.q[1] + a.q[1] * b.q[3] + a.q[2] * b.q[0] - a.q[0] * b.q[2];
+  const float z = a.q[3] * b.q[2] + a.q[2] * b.q[3] + a.q[0] * b.q[1] - a.q[1] * b.q[0];
+  const float w = a.q[3] * b.q[3] - a.q[0] * b.q[0] - a.q[1] * b.q[1] - a.q[2] * b.q[2];
+  const float n = sqrtf(x * x + y * y + z * z + w * w);
+  o.q[0] = x / n; o.q[1] = y / n; o.q[2] = z / n; o.q[3] = w / n;
+  g7_qact(a.q, b.t, t);
+  for (int i = 0; i < 3; i++) o.t[i] = a.t[i] + t[i];
+  return o;
+}
+/* transform of one pixel: Gij = poses[j] * poses[i].inv(), iproj, act4, proj */
+static void transform_px(const float* Pi, const float* Pj, const float* Ki, const float* Kj,
+                         float x, float y, float d, int tonly, float* out, float* Z) {
+  g7f gij = g7_reload(g7_mul(g7_load(Pj), g7_reload(g7_inv(g7_load(Pi)))));
+  float X0[4], p[3];
+  if (tonly) { gij.q[0] = gij.q[1] = gij.q[2] = 0.0f; gij.q[3] = 1.0f; }
+  X0[0] = (x - Ki[2]) / Ki[0];
+  X0[1] = (y - Ki[3]) / Ki[1];
+  X0[2] = 1.0f;
+  X0[3] = d;
+  g7_qact(gij.q, X0, p);
+  {
+    const float X = p[0] + gij.t[0] * X0[3], Y = p[1] + gij.t[1] * X0[3];
+    const float Zz = p[2] + gij.t[2] * X0[3];
+    const float inv = 1.0f / (Zz < 0.1f ? 0.1f : Zz);
+    out[0] = Kj[0] * (inv * X) + Kj[2];
+    out[1] = Kj[1] * (inv * Y) + Kj[3];
+    *Z = Zz;
+  }
+}
+
+/* flow[e * npx + p] = flow_mag of pixel p of patch kk[e] from frame ii[e] to
+   jj[e]; valid = Z1 > 0.2.  px0 >= 0 selects one pixel (patches[..., r, c]
+   with px0 = r * P + c, edges_loop), else all P*P pixels (motionmag). */
+ORC_API int orc_flow_mag(const float* poses, const float* patches, const float* intr, int P,
+                         const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int px0,
+                         float beta, float* flow, uint8_t* valid) {
+  const int PP = P * P, npx = px0 >= 0 ? 1 : PP;
+  for (int e = 0; e < E; e++) {
+    const int64_t a = ii[e], b = jj[e];
+    const float* pk = patches + kk[e] * 3 * PP;
+    for (int q = 0; q < npx; q++) {
+      const int px = px0 >= 0 ? px0 : q;
+      float c0[2], c1[2], c2[2], z0, z1, z2, a0, a1, b0, b1, f1, f2;
+      transform_px(poses + 7 * a, poses + 7 * a, intr + 4 * a, intr + 4 * a, pk[px], pk[PP + px],
+                   pk[2 * PP + px], 0, c0, &z0);
+      transform_px(poses + 7 * a, poses + 7 * b, intr + 4 * a, intr + 4 * b, pk[px], pk[PP + px],
+                   pk[2 * PP + px], 0, c1, &z1);
+      transform_px(poses + 7 * a, poses + 7 * b, intr + 4 * a, intr + 4 * b, pk[px], pk[PP + px],
+                   pk[2 * PP + px], 1, c2, &z2);
+      a0 = c1[0] - c0[0]; a1 = c1[1] - c0[1];
+      b0 = c2[0] - c0[0]; b1 = c2[1] - c0[1];
+      f1 = sqrtf(a0 * a0 + a1 * a1);
+      f2 = sqrtf(b0 * b0 + b1 * b1);
+      flow[(size_t)e * npx + q] = beta * f1 + (1.0f - beta) * f2;
+      valid[(size_t)e * npx + q] = z1 > 0.2f;
+    }
+  }
+  return 0;
+}
+
+/* SE3(a) * SE3(b).inv() in fp32 (dpvo.py:630, pg.delta) */
+ORC_API int orc_se3_mul_inv(const float* a, const float* b, float* out) {
+  g7f g = g7_mul(g7_load(a), g7_reload(g7_inv(g7_load(b))));
+  for (int i = 0; i < 3; i++) out[i] = g.t[i];
+  for (int i = 0; i < 4; i++) out[3 + i] = g.q[i];
+  return 0;
+}

@@ -281,3 +281,148 @@ def solve_system(J_Ginv_i, J_Ginv_j, ii, jj, res, ep, lm, freen):
         y = np.linalg.solve(L, b[:f])
         delta[:f] = np.linalg.solve(L.T, y)
     return delta.astype(np.float32).reshape(n, 7)
+
+
+# ---------------------------------------------------------------- keyframe / edges_loop
+def flow_mag(poses, patches, intrinsics, ii, jj, kk, beta=0.5, pixel=None):
+    """projective_ops.flow_mag (projective_ops.py:120-130) in fp32 op by op
+    (orc_flow_mag).  patches [N, 3, P, P]; pixel=(r, c) selects
+    patches[..., r, c] (edges_loop, patchgraph.py:79) -> ([E], [E]) else
+    ([E, P, P] flow, valid)."""
+    poses = _f32(poses).reshape(-1, 7)
+    P = np.shape(patches)[-1]
+    patches = _f32(patches).reshape(-1, 3, P, P)
+    intr = _f32(intrinsics).reshape(-1, 4)
+    ii, jj, kk = _i64(ii), _i64(jj), _i64(kk)
+    E = ii.shape[0]
+    px0 = -1 if pixel is None else pixel[0] * P + pixel[1]
+    npx = P * P if pixel is None else 1
+    flow = np.zeros(E * npx, np.float32)
+    val = np.zeros(E * npx, np.uint8)
+    _check(lib().orc_flow_mag(_p(poses), _p(patches), _p(intr), P, _p(ii), _p(jj), _p(kk), E,
+                              px0, ctypes.c_float(beta), _p(flow), _p(val)), "flow_mag")
+    if pixel is None:
+        return flow.reshape(E, P, P), val.reshape(E, P, P).astype(bool)
+    return flow, val.astype(bool)
+
+
+def _sum_f32(x):
+    """fp32 result of a sum accumulated in double in index order."""
+    return np.float32(np.sum(np.asarray(x, np.float64)))
+
+
+def motionmag(st, i, j):
+    """DPVO.motionmag (dpvo.py:586-599): mean flow_mag(beta 0.5) over the
+    pixels of the active edges i -> j; torch's mean = fp32 sum * (1 / N)."""
+    E = st["num_edges"]
+    ii, jj, kk = st["ii"][:E], st["jj"][:E], st["kk"][:E]
+    sel = (ii == i) & (jj == j)
+    if not sel.any():
+        return np.float32(0.0)
+    fl, _ = flow_mag(st["poses"], st["patches"], st["intrinsics"], ii[sel], jj[sel], kk[sel], 0.5)
+    return np.float32(_sum_f32(fl) * (np.float32(1.0) / np.float32(fl.size)))
+
+
+def keyframe(st, M, keyframe_index=4, keyframe_thresh=12.5, rings=None):
+    """DPVO.keyframe's frame drop (dpvo.py:601-673) on a numpy state dict
+    (copied): n, m, num_edges, ii/jj/kk/net/weight/target [max_edges, ...],
+    poses [N,7], patches [N*M,3,P,P], intrinsics [N,4], tstamps [N], plus any
+    per-frame array named in `rings` {name: ring} (ring 0: row = frame).
+    Returns (state, {"drop", "k", "mag", "delta"})."""
+    st = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in st.items()}
+    n = st["n"]
+    i, j = n - keyframe_index - 1, n - keyframe_index + 1
+    m0, m1 = motionmag(st, i, j), motionmag(st, j, i)
+    info = {"drop": False, "k": n - keyframe_index, "mag": (m0, m1), "delta": None}
+    if not ((float(m0) + float(m1)) / 2 < keyframe_thresh and i >= 0):
+        return st, info
+    k = n - keyframe_index
+    info["drop"] = True
+    info["delta"] = (int(st["tstamps"][k]), int(st["tstamps"][k - 1]),
+                     se3_mul_inv(st["poses"][k], st["poses"][k - 1]))
+    E = st["num_edges"]
+    ii, jj = st["ii"][:E], st["jj"][:E]
+    keep = ~((ii == k) | (jj == k))
+    ne = int(keep.sum())
+    for name in ("ii", "jj", "kk", "net", "weight", "target"):
+        if name in st:
+            st[name][:ne] = st[name][:E][keep]
+    st["num_edges"] = ne
+    ii, jj, kk = st["ii"][:ne], st["jj"][:ne], st["kk"][:ne]
+    mi, mj = ii > k, jj > k
+    kk[mi] -= M
+    ii[mi] -= 1
+    jj[mj] -= 1
+    frames = {"poses": 0, "intrinsics": 0, "tstamps": 0}
+    frames.update(rings or {})
+    for name, ring in frames.items():
+        a = st[name]
+        for f in range(k, n - 1):
+            src, dst = (f + 1, f) if not ring else ((f + 1) % ring, f % ring)
+            a[dst] = a[src]
+    pa = st["patches"].reshape(-1, M, *st["patches"].shape[1:])
+    for f in range(k, n - 1):
+        pa[f] = pa[f + 1]
+    st["n"] = n - 1
+    st["m"] = st["m"] - M
+    return st, info
+
+
+def se3_mul_inv(a, b):
+    """lietorch SE3(a) * SE3(b).inv() in fp32 (se3.h:325-336), 7 floats."""
+    out = np.zeros(7, np.float32)
+    _check(lib().orc_se3_mul_inv(_p(_f32(a)), _p(_f32(b)), _p(out)), "se3_mul_inv")
+    return out
+
+
+def reduce_edges(flow, ii, jj, max_num_edges=1000, nms=1):
+    """loop_closure/optim_utils.py:24-60.  Candidates in ascending flow order
+    (ties by index: a stable argsort; numba's argsort is not stable, exact
+    fp32 ties between distinct groups are the only case it could differ)."""
+    es = []
+    if len(ii) == 0:
+        return np.zeros((0, 2), np.int64)
+    Ni, Nj = int(ii.max()) + 1, int(jj.max()) + 1
+    ignore = np.zeros((Ni, Nj), bool)
+    for idx in np.argsort(flow, kind="stable"):
+        if len(es) + 1 > max_num_edges:
+            break
+        i, j, mag = int(ii[idx]), int(jj[idx]), flow[idx]
+        if j - i < 30 or mag >= 1000 or ignore[i, j]:
+            continue
+        es.append((i, j))
+        for di in range(-nms, nms + 1):
+            if 0 <= i + di < Ni:
+                ignore[i + di, j] = True
+    return np.asarray(es, np.int64).reshape(-1, 2)
+
+
+def edges_loop(poses, patches, intrinsics, ix, n, M, removal_window=20, max_edge_age=1000,
+               global_opt_freq=15, keyframe_index=4, backend_thresh=64.0, max_num_edges=1000,
+               nms=1):
+    """PatchGraph.edges_loop (patchgraph.py:65-91) -> (kk, jj) int64.
+    Group sums accumulate in double in patch order, then fp32 (the
+    reference's torch sum is unordered fp32)."""
+    l = n - removal_window
+    if l <= 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    jr = np.arange(n - global_opt_freq, n - keyframe_index)
+    kr = np.arange(max(l - max_edge_age, 0) * M, l * M)
+    jj, kk = np.meshgrid(jr, kr, indexing="ij")
+    jj, kk = jj.reshape(-1), kk.reshape(-1)
+    ix = np.asarray(ix, np.int64)
+    ii = ix[kk]
+    if len(kk) == 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    fl, val = flow_mag(poses, patches, intrinsics, ii, jj, kk, 0.5, pixel=(1, 1))
+    G = len(kk) // M
+    fl, val = fl.reshape(G, M), val.reshape(G, M)
+    s = np.array([_sum_f32(np.where(val[g], fl[g], 0.0)) for g in range(G)], np.float32)
+    c = val.sum(1).astype(np.float32)
+    fm = np.where(c > M * 0.75, s / np.maximum(c, np.float32(1)), np.float32(np.inf))
+    fm = fm.astype(np.float32)
+    mask = fm < backend_thresh
+    es = reduce_edges(fm[mask], ii[::M][mask], jj[::M][mask], max_num_edges, nms)
+    kk = (es[:, 0][:, None] * M + np.arange(M)[None]).reshape(-1)
+    jj = np.repeat(es[:, 1], M)
+    return kk.astype(np.int64), jj.astype(np.int64)

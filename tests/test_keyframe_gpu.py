@@ -1,0 +1,265 @@
+"""DPVO.keyframe's frame drop and PatchGraph.edges_loop on the device
+(csrc/keyframe.hip + pg.hip) vs the restatement in
+oracle/oracle.py (keyframe: dpvo.py:586-673; edges_loop: patchgraph.py:65-91
+with reduce_edges, loop_closure/optim_utils.py:24-60; flow_mag:
+projective_ops.py:120-130 in fp32 op by op, orc_flow_mag).
+
+* motion magnitudes, the drop decision, the edge list after removal and
+  index shift, every shifted per-frame array (incl. ring buffers and a
+  byte-sized array), the counters and the pg.delta record: bit-identical,
+  for a dropped and a kept frame;
+* edges_loop: per-group flow values bit-identical, the selected (kk, jj) and
+  count identical, the last_global_ba gate of dpvo.py:984-988;
+* everything runs without a host sync (the decision never leaves the
+  device) and replays from a captured graph."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _quat(axis, ang):
+    axis = np.asarray(axis, np.float64)
+    axis = axis / np.linalg.norm(axis)
+    return np.concatenate([np.sin(ang / 2) * axis, [np.cos(ang / 2)]])
+
+
+def _scene(rng, N, M, P, motion, n):
+    """poses (world->camera, lietorch [t, q]) along x with step `motion`,
+    small rotations; patches inside a 160 x 120 image with inverse depth in
+    [0.2, 1]."""
+    poses = np.zeros((N, 7), np.float32)
+    for f in range(N):
+        q = _quat(rng.normal(size=3), 0.01 * rng.normal())
+        poses[f, :3] = [-motion[f] if f < n else 0.0, 0.01 * rng.normal(), 0.01 * rng.normal()]
+        poses[f, 3:] = q
+    pts = np.zeros((N * M, 3, P, P), np.float32)
+    cx = rng.uniform(10, 150, N * M)
+    cy = rng.uniform(10, 110, N * M)
+    off = np.arange(P) - P // 2
+    pts[:, 0] = cx[:, None, None] + off[None, None, :]
+    pts[:, 1] = cy[:, None, None] + off[None, :, None]
+    pts[:, 2] = rng.uniform(0.2, 1.0, N * M)[:, None, None]
+    intr = np.tile(np.array([100.0, 100.0, 80.0, 60.0], np.float32), (N, 1))
+    return poses, pts, intr
+
+
+def _edges(n, M, r=3):
+    ii, jj, kk = [], [], []
+    for a in range(n):
+        for b in range(max(0, a - r), min(n, a + r + 1)):
+            for m in range(M):
+                ii.append(a)
+                jj.append(b)
+                kk.append(a * M + m)
+    return np.array(ii, np.int64), np.array(jj, np.int64), np.array(kk, np.int64)
+
+
+@pytest.mark.parametrize("drop", [True, False])
+def test_keyframe_frame_drop_matches_restatement(gpu, drop):
+    from dpvo_amd.patchgraph import DevicePatchGraph
+
+    rng = np.random.default_rng(7 if drop else 8)
+    N, M, P, n, DIM, pmem = 32, 10, 3, 20, 16, 6
+    # cumulative x motion: tiny steps around the candidate frame when dropping
+    step = np.where((np.arange(N) >= 14) & (np.arange(N) <= 18), 0.002 if drop else 0.5, 0.05)
+    motion = np.cumsum(step)
+    poses, pts, intr = _scene(rng, N, M, P, motion, n)
+    ii, jj, kk = _edges(n, M)
+    E, ME = len(ii), 4096
+    net = rng.normal(size=(E, DIM)).astype(np.float32)
+    weight = rng.uniform(size=(E, 2)).astype(np.float32)
+    target = rng.normal(size=(E, 2)).astype(np.float32)
+    tstamps = (np.arange(N) * 3 + 1).astype(np.int64)
+    gmap = rng.normal(size=(pmem, M, 4, P, P)).astype(np.float32)
+    colors = rng.integers(0, 255, size=(N, M, 3), dtype=np.uint8)  # 30 B per frame
+
+    pg = DevicePatchGraph(max_edges=ME, DIM=DIM, device=gpu)
+    ix = torch.arange(N * M, device=gpu) // M
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+    pg.append_factors(ix, T(kk), T(jj))
+    pg.net[0, :E] = T(net)
+    pg.weight[0, :E] = T(weight)
+    pg.target[0, :E] = T(target)
+    dP, dK, dI, dts = T(poses), T(pts), T(intr), T(tstamps)
+    dg, dc = T(gmap), T(colors)
+    st = torch.tensor([n, n * M], dtype=torch.int32, device=gpu)
+    log = (torch.zeros(4, 7, device=gpu), torch.zeros(4, 2, dtype=torch.long, device=gpu),
+           torch.zeros(1, dtype=torch.int32, device=gpu))
+    kf, mag = pg.keyframe(st, dP, dK, dI, M, frames=[dg, dc], rings=[pmem, 0], tstamps=dts,
+                          delta=log)
+    torch.cuda.synchronize()
+
+    ref_st = {"n": n, "m": n * M, "num_edges": E, "poses": poses, "patches": pts,
+              "intrinsics": intr, "tstamps": tstamps, "gmap": gmap, "colors": colors}
+    for name, a in (("ii", ii), ("jj", jj), ("kk", kk), ("net", net), ("weight", weight),
+                    ("target", target)):
+        full = np.zeros((ME,) + a.shape[1:], a.dtype)
+        full[:E] = a
+        ref_st[name] = full
+    rs, info = oracle.keyframe(ref_st, M, rings={"gmap": pmem, "colors": 0})
+    assert info["drop"] == drop
+    m = mag.cpu().numpy()
+    assert m[0] == info["mag"][0] and m[1] == info["mag"][1], (m, info["mag"])
+    assert kf.cpu().tolist() == [int(drop), n - 4]
+    ne = rs["num_edges"]
+    assert pg.num_edges == ne and pg.errors == 0
+    if drop:
+        assert ne < E
+    for name in ("ii", "jj", "kk"):
+        np.testing.assert_array_equal(getattr(pg, name)[:ne].cpu().numpy(), rs[name][:ne], name)
+    for name in ("net", "weight", "target"):
+        np.testing.assert_array_equal(getattr(pg, name)[0, :ne].cpu().numpy(), rs[name][:ne],
+                                      name)
+    assert st.cpu().tolist() == [rs["n"], rs["m"]]
+    np.testing.assert_array_equal(dP.cpu().numpy(), rs["poses"])
+    np.testing.assert_array_equal(dK.cpu().numpy(), rs["patches"])
+    np.testing.assert_array_equal(dI.cpu().numpy(), rs["intrinsics"])
+    np.testing.assert_array_equal(dts.cpu().numpy(), rs["tstamps"])
+    np.testing.assert_array_equal(dg.cpu().numpy(), rs["gmap"])
+    np.testing.assert_array_equal(dc.cpu().numpy(), rs["colors"])
+    cnt = int(log[2].item())
+    assert cnt == int(drop)
+    if drop:
+        t1, t0, dp = info["delta"]
+        assert log[1][0].cpu().tolist() == [t1, t0]
+        np.testing.assert_array_equal(log[0][0].cpu().numpy(), dp)
+
+
+def _loop_scene(rng, N, M, P, n, period=40):
+    """a camera circling with `period` frames per lap: frame pairs one lap
+    apart see the same view (small flow), others do not."""
+    poses = np.zeros((N, 7), np.float32)
+    for f in range(N):
+        th = 2 * np.pi * f / period
+        R = _quat([0, 1, 0], -th)
+        c = np.array([0.6 * np.sin(th), 0.0, 0.6 * (1 - np.cos(th))])
+        # world->camera: t = -R c (rotation about y applied to the centre)
+        ca, sa = np.cos(-th), np.sin(-th)
+        Rm = np.array([[ca, 0, sa], [0, 1, 0], [-sa, 0, ca]])
+        poses[f, :3] = -Rm @ c + 0.002 * rng.normal(size=3)
+        poses[f, 3:] = R
+    _, pts, intr = _scene(rng, N, M, P, np.zeros(N), 0)
+    pts[:, 2] = rng.uniform(0.5, 1.5, N * M)[:, None, None]
+    return poses, pts, intr
+
+
+@pytest.mark.parametrize("M,n,thresh", [(10, 120, 64.0), (96, 90, 64.0), (12, 200, 8.0)])
+def test_edges_loop_matches_restatement(gpu, M, n, thresh):
+    from dpvo_amd.patchgraph import DevicePatchGraph
+
+    rng = np.random.default_rng(M + n)
+    N, P = n + 8, 3
+    poses, pts, intr = _loop_scene(rng, N, M, P, n)
+    ix = np.repeat(np.arange(N), M).astype(np.int64)
+    pg = DevicePatchGraph(max_edges=20000, DIM=16, device=gpu, net=False)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+    st = torch.tensor([n, n * M], dtype=torch.int32, device=gpu)
+    kk, jj, cnt = pg.edges_loop(T(poses), T(pts), T(intr), T(ix), st, N, M,
+                                backend_thresh=thresh)
+    torch.cuda.synchronize()
+    rk, rj = oracle.edges_loop(poses, pts, intr, ix, n, M, backend_thresh=thresh)
+    c = int(cnt.item())
+    assert c == len(rk) and c > 0
+    np.testing.assert_array_equal(kk[:c].cpu().numpy(), rk)
+    np.testing.assert_array_equal(jj[:c].cpu().numpy(), rj)
+    # the append of the device count gives ii = ix[kk]
+    pg.append_factors_dev(T(ix), kk, jj, cnt)
+    assert pg.num_edges == c
+    np.testing.assert_array_equal(pg.ii[:c].cpu().numpy(), ix[rk])
+
+
+def test_edges_loop_group_values_bit_exact(gpu):
+    """the per-group flow magnitudes (the work buffer's first ng floats)
+    equal the restatement's fp32 values bit for bit."""
+    from dpvo_amd.patchgraph import DevicePatchGraph
+
+    rng = np.random.default_rng(3)
+    M, n, P = 20, 70, 3
+    N = n + 4
+    poses, pts, intr = _loop_scene(rng, N, M, P, n)
+    ix = np.repeat(np.arange(N), M).astype(np.int64)
+    pg = DevicePatchGraph(max_edges=100, DIM=16, device=gpu, net=False)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+    st = torch.tensor([n, n * M], dtype=torch.int32, device=gpu)
+    out = (torch.empty(1000 * M, dtype=torch.long, device=gpu),
+           torch.empty(1000 * M, dtype=torch.long, device=gpu),
+           torch.zeros(1, dtype=torch.int32, device=gpu),
+           torch.empty(pg._ext.edges_loop_work_floats(), device=gpu))
+    pg.edges_loop(T(poses), T(pts), T(intr), T(ix), st, N, M, out=out)
+    torch.cuda.synchronize()
+    l = n - 20
+    jr = np.arange(n - 15, n - 4)
+    kr = np.arange(0, l * M)
+    J, K = np.meshgrid(jr, kr, indexing="ij")
+    J, K = J.reshape(-1), K.reshape(-1)
+    fl, val = oracle.flow_mag(poses, pts, intr, ix[K], J, K, 0.5, pixel=(1, 1))
+    G = len(K) // M
+    fl, val = fl.reshape(G, M), val.reshape(G, M)
+    s = np.array([oracle._sum_f32(np.where(val[g], fl[g], 0.0)) for g in range(G)], np.float32)
+    c = val.sum(1).astype(np.float32)
+    ref = np.where(c > M * 0.75, s / np.maximum(c, np.float32(1)), np.float32(np.inf))
+    got = out[3][:G].cpu().numpy()
+    np.testing.assert_array_equal(got.view(np.uint32), ref.astype(np.float32).view(np.uint32))
+
+
+def test_edges_loop_gate_and_graph_replay(gpu):
+    """dpvo.py:984-988 on the device: nothing while n - last_global_ba <
+    GLOBAL_OPT_FREQ; last_global_ba = n once edges are found.  The
+    edges_loop + append pair captured in a graph replays with the device
+    frame counter moving underneath it."""
+    from dpvo_amd.patchgraph import DevicePatchGraph
+
+    rng = np.random.default_rng(11)
+    M, P, n0 = 10, 3, 100
+    N = n0 + 40
+    poses, pts, intr = _loop_scene(rng, N, M, P, N)
+    ix = np.repeat(np.arange(N), M).astype(np.int64)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+    dP, dK, dI, dix = T(poses), T(pts), T(intr), T(ix)
+    pg = DevicePatchGraph(max_edges=60000, DIM=16, device=gpu, net=False)
+    st = torch.tensor([n0, n0 * M], dtype=torch.int32, device=gpu)
+    last = torch.tensor([n0 - 10], dtype=torch.int32, device=gpu)
+    out = (torch.empty(1000 * M, dtype=torch.long, device=gpu),
+           torch.empty(1000 * M, dtype=torch.long, device=gpu),
+           torch.zeros(1, dtype=torch.int32, device=gpu),
+           torch.empty(pg._ext.edges_loop_work_floats(), device=gpu))
+
+    inc = torch.tensor([1, M], dtype=torch.int32, device=gpu)
+
+    def frame():
+        kk, jj, cnt = pg.edges_loop(dP, dK, dI, dix, st, N, M, last_global_ba=last, out=out)
+        pg.append_factors_dev(dix, kk, jj, cnt)
+        st.add_(inc)
+
+    # host model of the gate
+    exp_total, lb, n = 0, n0 - 10, n0
+    counts = []
+    for _ in range(3):
+        frame()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        frame()  # warm on the side stream
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        frame()
+    for _ in range(20):
+        g.replay()
+    torch.cuda.synchronize()
+    for f in range(3 + 1 + 20):
+        if n - lb >= 15:
+            rk, _ = oracle.edges_loop(poses, pts, intr, ix, n, M)
+            if len(rk):
+                lb = n
+            exp_total += len(rk)
+            counts.append(len(rk))
+        n += 1
+    assert int(st[0].item()) == n
+    assert int(last.item()) == lb
+    assert pg.num_edges == exp_total and exp_total > 0
+    assert sum(1 for c in counts if c) >= 2  # the gate opened more than once

@@ -41,7 +41,7 @@ def test_update_loop_runs_and_converges(gpu):
     assert st["corr_shape"] == (1, st["edges"], 7 * 7 * 9 * 2)
     # depths of patches observed in many windows: far closer to the truth than
     # the 0.6 initialisation (whose mean error is ~0.2)
-    init = float((h.gt_d[:n * M] - 0.6).abs().mean())
+    init = float((h.gt_patches[:n * M, 2, 1, 1] - 0.6).abs().mean())
     assert h.depth_error(n - 20, n - 12) < 0.25 * init, (h.depth_error(n - 20, n - 12), init)
     assert h.pose_error() < 0.05
 
@@ -124,3 +124,37 @@ def test_graph_replay_matches_eager(gpu):
     for k in ("ii", "jj", "kk"):
         assert torch.equal(getattr(a.pg, k)[:E], getattr(b.pg, k)[:E]), k
     assert a.check() == 0 and b.check() == 0
+
+
+def test_update_loop_with_device_keyframes(gpu):
+    """DPVO's update + keyframe() (dpvo.py:1013-1015) with the frame drop on
+    the device: frames are dropped, and every per-frame buffer moved with the
+    surviving frames -- the truth, the initial patches' pixel positions and the
+    feature rings at index i all belong to timestamp tstamps[i] -- and the BA
+    still converges."""
+    from dpvo_amd.update import UpdateHarness
+
+    M = 8
+    h = UpdateHarness(device=gpu, M=M, buffer=160, pose_noise=0.0, depth_init=0.6,
+                      keyframes=True)
+    for _ in range(70):
+        h.step()
+    n = h.n
+    assert h.dropped > 0 and n + h.dropped == h.t
+    assert int(h.delta[2].item()) == h.dropped
+    ts = h.tstamps[:n].cpu()
+    assert bool((ts[1:] > ts[:-1]).all()) and int(ts[-1]) == h.t - 1
+    tsd = ts.to(gpu)
+    assert torch.equal(h.gt_poses[:n], h.gt_poses_t[tsd])
+    rows = (tsd.view(-1, 1) * M + torch.arange(M, device=gpu)).view(-1)
+    assert torch.equal(h.gt_patches[:n * M], h.gt_patches_t[rows])
+    assert torch.equal(h.patches[:n * M, :2], h.init_patches_t[rows, :2])  # BA moves depth only
+    # the level-1 ring slot of the last frames holds that frame's features
+    for i in range(n - 5, n):
+        f = (0.25 * torch.sin(h.field + 0.37 * float(ts[i]))).to(h.feat_dtype)
+        assert torch.equal(h.pyr[0][0, i % h.mem], f), i
+    # a delta record: (t1, t0) of a dropped frame and its predecessor
+    t1, t0 = h.delta[1][0].tolist()
+    assert t1 > t0 and int((ts == t1).sum()) == 0
+    assert h.check() == 0
+    assert h.pose_error_scaled()[0] < 0.05
