@@ -848,7 +848,7 @@ void kf_shift(torch::Tensor kf, int64_t M, torch::Tensor st, torch::Tensor ii, t
 
 // PatchGraph.edges_loop (patchgraph.py:65-91) gated as dpvo.py:984-988
 void edges_loop(torch::Tensor poses, torch::Tensor patches, torch::Tensor intrinsics,
-                torch::Tensor ix, torch::Tensor st, int64_t n_cap,
+                torch::Tensor ix, int64_t M, torch::Tensor st, int64_t n_cap,
                 c10::optional<torch::Tensor> last_global_ba, int64_t removal_window,
                 int64_t max_edge_age, int64_t global_opt_freq, int64_t keyframe_index,
                 double backend_thresh, int64_t max_num_edges, int64_t nms, torch::Tensor work,
@@ -857,7 +857,8 @@ void edges_loop(torch::Tensor poses, torch::Tensor patches, torch::Tensor intrin
   TORCH_CHECK(work.scalar_type() == torch::kFloat32 &&
                   work.numel() >= (int64_t)dpvo_edges_loop_work_floats(),
               "work: float32[edges_loop_work_floats()]");
-  const int M = (int)patches.size(-4);
+  TORCH_CHECK(M > 0 && patches.numel() % (M * 3 * patches.size(-1) * patches.size(-1)) == 0,
+              "patches: [N * M, 3, P, P]");
   TORCH_CHECK(out_kk.numel() >= max_num_edges * M && out_jj.numel() >= max_num_edges * M,
               "out_kk / out_jj: max_num_edges x M");
   int32_t* lb = (last_global_ba && last_global_ba->defined())
@@ -865,7 +866,7 @@ void edges_loop(torch::Tensor poses, torch::Tensor patches, torch::Tensor intrin
                     : nullptr;
   check_status(dpvo_edges_loop(poses.data_ptr<float>(), patches.data_ptr<float>(),
                                intrinsics.data_ptr<float>(), idx64(ix, "ix").data_ptr<int64_t>(),
-                               (int)patches.size(-1), M, dev_scalar(st, "st"), (int)n_cap, lb,
+                               (int)patches.size(-1), (int)M, dev_scalar(st, "st"), (int)n_cap, lb,
                                (int)removal_window, (int)max_edge_age, (int)global_opt_freq,
                                (int)keyframe_index, (float)backend_thresh, (int)max_num_edges,
                                (int)nms, work.data_ptr<float>(), out_kk.data_ptr<int64_t>(),

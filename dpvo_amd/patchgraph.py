@@ -174,7 +174,8 @@ class DevicePatchGraph:
                    torch.zeros(1, dtype=torch.int32, device=dev),
                    torch.empty(self._ext.edges_loop_work_floats(), device=dev))
         kk, jj, cnt, work = out
-        self._ext.edges_loop(poses, patches, intrinsics, ix, st, int(n_cap), last_global_ba,
+        self._ext.edges_loop(poses, patches, intrinsics, ix, int(M), st, int(n_cap),
+                             last_global_ba,
                              int(removal_window), int(max_edge_age), int(global_opt_freq),
                              int(keyframe_index), float(backend_thresh), int(max_num_edges),
                              int(nms), work, kk, jj, cnt)

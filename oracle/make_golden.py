@@ -21,6 +21,16 @@ Fixtures (numpy .npz, inputs + expected outputs, seeded):
                         lietorch_backends is provided by the build's own CPU SE3
                         restatement (oracle/dpvo_oracle.c), torch_scatter by index_add_.
   transform_*.npz      dpvo/projective_ops.py transform (53-113) coords + Jacobians.
+  keyframe_a.npz       dpvo/projective_ops.py flow_mag (120-130) on DPVO-window edges
+                        (motionmag's input, dpvo.py:586-599) and at patch pixel (1, 1)
+                        on the edges_loop candidates; the edges_loop composition
+                        (patchgraph.py:74-91: flow_mag -> einops reduce -> mask ->
+                        reduce_edges) and reduce_edges (loop_closure/optim_utils.py:
+                        24-60) on a crafted case.  optim_utils is imported with numba
+                        (absent) replaced by a pass-through njit and pypose (absent,
+                        unused by reduce_edges) by an empty module.
+
+    python oracle/make_golden.py [corr] [patchify] [ba] [keyframe]   (default: all)
 """
 from __future__ import annotations
 
@@ -271,14 +281,114 @@ def make_ba(ref_ba, ref_pops, SE3):
         print(name, "E", len(G["ii"]), "t1", t1)
 
 
+def load_optim_utils():
+    """loop_closure/optim_utils.py with numba / pypose absent: njit runs the
+    plain Python function (reduce_edges is pure numpy-style Python)."""
+    nb = types.ModuleType("numba")
+    nb.bool_ = np.bool_
+
+    def njit(*a, **k):
+        if a and callable(a[0]):
+            return a[0]
+        return lambda f: f
+
+    nb.njit = njit
+    sys.modules.setdefault("numba", nb)
+    pp = types.ModuleType("pypose")
+    pp.__getattr__ = lambda name: type(name, (), {})  # annotations only (pp.SE3, ...)
+    sys.modules.setdefault("pypose", pp)
+    path = os.path.join(REF, "dpvo", "loop_closure", "optim_utils.py")
+    spec = importlib.util.spec_from_file_location("ref_optim_utils", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def loop_scene(seed, N, M, P=3, period=40):
+    """a camera circling with `period` frames per lap (revisits -> loop edges)."""
+    rng = np.random.default_rng(seed)
+    poses = np.zeros((N, 7), np.float32)
+    for f in range(N):
+        th = 2 * np.pi * f / period
+        c = np.array([0.6 * np.sin(th), 0.0, 0.6 * (1 - np.cos(th))])
+        ca, sa = np.cos(-th), np.sin(-th)
+        Rm = np.array([[ca, 0, sa], [0, 1, 0], [-sa, 0, ca]])
+        poses[f, :3] = -Rm @ c + 0.002 * rng.normal(size=3)
+        poses[f, 3:] = [0.0, np.sin(-th / 2), 0.0, np.cos(-th / 2)]
+    pts = np.zeros((N * M, 3, P, P), np.float32)
+    cx, cy = rng.uniform(10, 150, N * M), rng.uniform(10, 110, N * M)
+    off = np.arange(P) - P // 2
+    pts[:, 0] = cx[:, None, None] + off[None, None, :]
+    pts[:, 1] = cy[:, None, None] + off[None, :, None]
+    pts[:, 2] = rng.uniform(0.5, 1.5, N * M)[:, None, None]
+    intr = np.tile(np.array([100.0, 100.0, 80.0, 60.0], np.float32), (N, 1))
+    return poses, pts, intr
+
+
+def make_keyframe(ref_pops, SE3):
+    from einops import reduce
+
+    ou = load_optim_utils()
+    M, n, P = 10, 120, 3
+    N = n + 8
+    poses, pts, intr = loop_scene(71, N, M, P)
+    T = torch.from_numpy
+    Ps, Ks, Is = SE3(T(poses).unsqueeze(0)), T(pts).unsqueeze(0), T(intr).unsqueeze(0)
+    # motionmag input: DPVO-window edges (frames within 3 of each other)
+    ei, ej, ek = [], [], []
+    for a in range(n - 12, n):
+        for b in range(max(0, a - 3), min(n, a + 4)):
+            for m in range(M):
+                ei.append(a), ej.append(b), ek.append(a * M + m)
+    ei, ej, ek = (torch.tensor(v) for v in (ei, ej, ek))
+    flow, val = ref_pops.flow_mag(Ps, Ks, Is, ei, ej, ek, beta=0.5)
+    # edges_loop (patchgraph.py:74-91), RW 20, GOF 15, KI 4, AGE 1000, thresh 64
+    l = n - 20
+    jr = torch.arange(n - 15, n - 4)
+    kr = torch.arange(max(l - 1000, 0) * M, l * M)
+    jj, kk = (t.reshape(-1) for t in torch.meshgrid(jr, kr, indexing="ij"))
+    ix = torch.arange(N).repeat_interleave(M)
+    ii = ix[kk]
+    fmg, lval = ref_pops.flow_mag(Ps, Ks[..., 1, 1].view(1, -1, 3, 1, 1), Is, ii, jj, kk, beta=0.5)
+    fsum = reduce(fmg * lval, "1 (fl M) 1 1 -> fl", "sum", M=M).float()
+    nval = reduce(lval, "1 (fl M) 1 1 -> fl", "sum", M=M).clamp(min=1)
+    fm = torch.where(nval > (M * 0.75), fsum / nval, torch.inf)
+    mask = fm < 64.0
+    es = ou.reduce_edges(fm[mask].numpy(), ii[::M][mask].numpy(), jj[::M][mask].numpy(),
+                         max_num_edges=1000, nms=1)
+    edges = torch.as_tensor(es)
+    from einops import repeat
+
+    li, lj = repeat(edges, "E ij -> ij E M", M=M, ij=2)
+    lk = li.mul(M) + torch.arange(M)
+    # reduce_edges on a crafted case: inf, >= 1000, j - i < 30, NMS rows, cap
+    rf = np.array([5.0, 1.0, np.inf, 2.0, 1500.0, 3.0, 0.5, 4.0, 2.5, 0.25], np.float32)
+    ri = np.array([10, 11, 12, 40, 3, 12, 50, 2, 9, 60], np.int64)
+    rj = np.array([60, 60, 60, 90, 60, 61, 70, 61, 60, 95], np.int64)
+    res = [ou.reduce_edges(rf, ri, rj, max_num_edges=cap, nms=1) for cap in (1000, 3)]
+    np.savez_compressed(
+        os.path.join(OUT, "keyframe_a.npz"), poses=poses, patches=pts, intrinsics=intr, M=M, n=n,
+        ei=ei.numpy(), ej=ej.numpy(), ek=ek.numpy(), flow=flow[0].numpy(), valid=val[0].numpy(),
+        loop_flow=fm.numpy(), loop_kk=lk.flatten().numpy(), loop_jj=lj.flatten().numpy(),
+        re_flow=rf, re_ii=ri, re_jj=rj, re_es=res[0], re_es_cap3=res[1])
+    print("keyframe_a loop edges", len(es), "flow edges", len(ei))
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(4)
-    cm = load_corr_module()
-    make_corr(cm)
-    make_patchify(cm)
-    ref_ba, ref_pops, SE3 = load_ba_module()
-    make_ba(ref_ba, ref_pops, SE3)
+    which = set(sys.argv[1:]) or {"corr", "patchify", "ba", "keyframe"}
+    cm = load_corr_module() if which & {"corr", "patchify"} else None
+    if "corr" in which:
+        make_corr(cm)
+    if "patchify" in which:
+        make_patchify(cm)
+    if which & {"ba", "keyframe"}:
+        ref_ba, ref_pops, SE3 = load_ba_module()
+        if "ba" in which:
+            make_ba(ref_ba, ref_pops, SE3)
+        if "keyframe" in which:
+            make_keyframe(ref_pops, SE3)
 
 
 if __name__ == "__main__":
