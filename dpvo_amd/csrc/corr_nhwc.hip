@@ -434,7 +434,13 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
       const T* s = base + pix(ai) + CorrT<T>::kLaneCh * aq;
 #pragma unroll
       for (int h = 0; h < V; h++)
+#if defined(CORR_DIAG_NO_LOAD)  // diagnostic builds only: no tile loads
+        dst[h] = (u32x4){(unsigned)h, (unsigned)i, 0u, 0u};
+#elif defined(CORR_NT_LOADS)  // diagnostic builds: streaming (non-temporal) tile loads
+        dst[h] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s + (kHalf ? 8 * h : 16 * h)));
+#else
         dst[h] = *reinterpret_cast<const u32x4*>(s + (kHalf ? 8 * h : 16 * h));
+#endif
     }
   };
   u32x4 ring[kRing][V];
@@ -508,7 +514,14 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
           }
         }
       };
+#ifndef CORR_DIAG_NO_MMA  // diagnostic builds only (timing of the rest of the tile loop)
       if (live) mma(cur);
+#else
+      if (live) {
+        acc0[0] = __builtin_bit_cast(float, cur[0].x);
+        acc1[0] = __builtin_bit_cast(float, cur[V - 1].w);
+      }
+#endif
       {
         // refill this slot with tile i + kRing (past the end: the last tile again,
         // never used); unconditional, so every path into the next group has the

@@ -4,7 +4,7 @@
 // pyramid, levels [1,2,4,8], 160x120 level-1 maps, 128 channels.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I dpvo_amd/csrc \
 //         scripts/micro/corr_bench.hip -o scripts/micro/corr_bench
-//   ./scripts/micro/corr_bench [ordered=1]
+//   ./scripts/micro/corr_bench [ordered=1] [first level] [levels] [edges] [parts=2]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -101,7 +101,8 @@ int main(int argc, char** argv) {
   hipMalloc(&dord, E * 4);
   hipMemcpy(dord, order.data(), E * 4, hipMemcpyHostToDevice);
   hipMalloc(&dout, (size_t)E * 49 * 9 * L * 4);
-  hipMalloc(&dst, (size_t)E * 16 * 8);
+  const int parts = 1;
+  hipMalloc(&dst, (size_t)E * 2 * 16 * 8);
   hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dst, sizeof(dst));
   // optional level subset: corr_bench <ordered> <first level> <count>
   const int l0 = argc > 2 ? atoi(argv[2]) : 0, Lr = argc > 3 ? atoi(argv[3]) : L;
@@ -118,7 +119,7 @@ int main(int argc, char** argv) {
   hipEventCreate(&b);
   std::vector<float> ms;
   for (int r = 0; r < 60; r++) {
-    hipMemset(dst, 0, (size_t)E * 16 * 8);
+    hipMemset(dst, 0, (size_t)E * 2 * 16 * 8);
     hipEventRecord(a, 0);
     int st = dpvo_corr_forward_levels_nhwc_ordered(gmap, f2, H2r, W2r, scr, Lr, dco, dii, djj,
                                                    ordered ? dord : nullptr, 1, E, C, P, P,
@@ -134,9 +135,14 @@ int main(int argc, char** argv) {
     if (r >= 10) ms.push_back(t);
   }
   std::sort(ms.begin(), ms.end());
-  printf("ordered=%d kernel median %.1f us\n", ordered, 1e3 * ms[ms.size() / 2]);
-  std::vector<int64_t> h((size_t)E * 16);
+  printf("ordered=%d parts=%d kernel median %.1f us\n", ordered, parts, 1e3 * ms[ms.size() / 2]);
+  std::vector<int64_t> h((size_t)E * 2 * 16);
   hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost);
+  if (parts == 2) {  // per (edge, part) stamps: analyse the waves as units
+    std::vector<int64_t> h2((size_t)E * 16, 0);
+    for (int e = 0; e < E; e++) for (int k = 0; k < 16; k++) h2[(size_t)e * 16 + k] = h[(size_t)(2 * e) * 16 + k];
+    h.swap(h2);
+  }
   int64_t t0 = INT64_MAX, t1 = 0;
   for (int e = 0; e < E; e++) {
     t0 = std::min(t0, h[(size_t)e * 16]);
