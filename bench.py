@@ -4,7 +4,8 @@ synthetic patch graph -- 96 patches x 2048 edges, p=3, 4-level pyramid
 
 One step = one DPVO update iteration with all inputs resident in HBM:
   frame     insertion of one new frame into the channels-last pyramid ring
-  F-REPROJ  (cuda_ba.reproject, E x 9 points)
+  F-REPROJ  (cuda_ba.reproject, E x 9 points; the same launch inserts the
+            frame, orders the edges for A-CORR and plans the BA)
   A-CORR    (all 4 levels in one launch, cuda_corr.forward_levels)
   F-BA      (cuda_ba.forward, 2 iterations, poses/patches updated in place)
 By default every kernel is launched from Python each step, as DPVO runs; the
@@ -184,6 +185,9 @@ def main():
     ap.add_argument("--separate-plan", action="store_true",
                     help="launch the BA edge grouping as its own kernel after A-CORR (default: "
                          "inside the reprojection launch, fastba.reproject(plan_window=...))")
+    ap.add_argument("--separate-insert", action="store_true",
+                    help="insert the frame into the pyramid as its own launch (default: inside "
+                         "the reprojection + plan launch, on the CUs those leave idle)")
     ap.add_argument("--sharded", action="store_true",
                     help="cfg4 global BA, edge-sharded over the ranks (one RCCL all_reduce of "
                          "the packed (S, y) per iteration); --config picks the large graph")
@@ -241,6 +245,7 @@ def main():
     plan_stream = torch.cuda.Stream()
     fused_plan = (not args.overlap and not args.separate_plan
                   and fastba.cuda_ba.plan_supported(int(D.ii.numel()), 1, G.F, P))
+    fused_insert = fused_plan and not args.separate_insert
 
     def step(i=0, ev=None):
         cur = torch.cuda.current_stream()
@@ -255,10 +260,18 @@ def main():
             if ws is not None:
                 ws.record_stream(cur)
         slot = i % args.mem  # frame insertion (dpvo.py:__call__ -> ring buffer)
-        altcorr.insert_frame(pyr_nchw[0][0, slot], pyr, slot, levels)
+        if fused_insert:
+            # frame insertion + reprojection + A-CORR edge order + BA plan, one launch
+            coords, order, ws = fastba.reproject(
+                poses, patches, D.intrinsics, D.ii, D.jj, D.kk, mem=args.mem, plan_window=(1, G.F),
+                insert=(pyr_nchw[0][0, slot], [p[0, slot] for p in pyr], levels))
+        else:
+            altcorr.insert_frame(pyr_nchw[0][0, slot], pyr, slot, levels)
         # reprojection + the XCD-aware edge order (edges grouped by target
         # frame) in one launch; A-CORR processes each group on one XCD
-        if fused_plan:
+        if fused_insert:
+            pass
+        elif fused_plan:
             # ... and the BA edge grouping (reads ii / jj / kk only, fixed for
             # the update) as workgroup 0 of the same launch
             coords, order, ws = fastba.reproject(poses, patches, D.intrinsics, D.ii, D.jj, D.kk,
@@ -382,6 +395,8 @@ def main():
             "launch": "eager" if graph is None else "hipGraph replay of one captured step",
             "ba_plan": ("side stream, concurrent with A-CORR" if args.overlap else
                         "in the reprojection launch" if fused_plan else "inline (same stream)"),
+            "frame_insertion": ("in the reprojection + plan launch" if fused_insert else
+                                "own launch"),
             "config": {
                 "workload": f"{args.config}: {G.M} patches/frame x {G.E} edges, p={P}, "
                             f"{len(levels)}-level pyramid {levels}, "

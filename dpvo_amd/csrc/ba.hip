@@ -1061,6 +1061,13 @@ int ba_window_reproject_plan(const float* poses, const float* patches, const flo
                              int num_poses, int num_patches, int N2, float* coords, int* order,
                              int t0, int t1, char* scratch, int* status, void* stream,
                              const int* t0d);
+int ba_window_reproject_plan_insert(const float* poses, const float* patches,
+                                    const float* intrinsics, const int64_t* ii, const int64_t* jj,
+                                    const int64_t* kk, int E, int P, int num_poses,
+                                    int num_patches, int N2, float* coords, int* order, int t0,
+                                    int t1, char* scratch, int* status, const void* src,
+                                    void* const* dst, const int* scale, int L, int C, int H, int W,
+                                    int half, void* stream);
 int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
                   const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                   const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
@@ -1446,6 +1453,33 @@ DPVO_EXPORT int dpvo_reproject_ordered_plan(const float* poses, const float* pat
   return ba_window_reproject_plan(poses, patches, intrinsics, ii, jj, kk, E, P, num_poses,
                                   num_patches, N2, coords, (int*)order, t0, t1,
                                   (char*)workspace + base_bytes, w.meta + 1, stream, nullptr);
+}
+
+DPVO_EXPORT int dpvo_reproject_ordered_plan_insert(
+    const float* poses, const float* patches, const float* intrinsics, const int64_t* ii,
+    const int64_t* jj, const int64_t* kk, int E, int P, int num_poses, int num_patches, int N2,
+    float* coords, int32_t* order, int t0, int t1, void* workspace, size_t workspace_bytes,
+    const void* src, void* const* dst, const int* scale, int L, int C, int H, int W, int dtype,
+    void* stream) {
+  if (E <= 0) return DPVO_OK;
+  if (P <= 0 || num_poses <= 0 || num_patches <= 0 || !order || !coords || !poses || !patches ||
+      !intrinsics || !ii || !jj || !kk || !workspace || t1 < t0 || !src || !dst || !scale ||
+      L <= 0 || C <= 0 || H <= 0 || W <= 0)
+    return DPVO_ERR_INVALID;
+  if ((dtype != DPVO_F32 && dtype != DPVO_F16) || L > 4) return DPVO_ERR_UNSUPPORTED;
+  for (int l = 0; l < L; l++) {
+    if (!dst[l]) return DPVO_ERR_INVALID;
+    if (scale[l] != 1 && scale[l] != 2 && scale[l] != 4 && scale[l] != 8)
+      return DPVO_ERR_UNSUPPORTED;
+  }
+  if (!ba_window_supported(E, t1 - t0, P)) return DPVO_ERR_UNSUPPORTED;
+  if (workspace_bytes < dpvo_ba_workspace_bytes(E, t0, t1)) return DPVO_ERR_WORKSPACE;
+  BaWs w;
+  const size_t base_bytes = ba_layout(E, t1 - t0, (char*)workspace, &w);
+  return ba_window_reproject_plan_insert(poses, patches, intrinsics, ii, jj, kk, E, P, num_poses,
+                                         num_patches, N2, coords, (int*)order, t0, t1,
+                                         (char*)workspace + base_bytes, w.meta + 1, src, dst,
+                                         scale, L, C, H, W, dtype == DPVO_F16 ? 1 : 0, stream);
 }
 
 DPVO_EXPORT int dpvo_reproject_ordered_plan_dev(const float* poses, const float* patches,

@@ -35,6 +35,7 @@
 #include <mutex>
 
 #include "ba_solve.hpp"
+#include "pyr_insert.hpp"
 
 namespace dpvo {
 namespace {
@@ -396,6 +397,48 @@ __global__ void __launch_bounds__(kPT) reproject_plan_kernel(RArgs R, Plan plan)
   if (t >= R.E * PP) return;
   reproject_pixel(R.poses, R.patches, R.intrinsics, R.ii, R.jj, R.kk, t / PP, t % PP, R.P,
                   R.num_poses, R.num_patches, R.coords);
+}
+
+// The same launch with the insertion of the update's new frame into the
+// channels-last pyramid ring (dpvo.py __call__, before update()): its tiles
+// (two 256-thread tiles per workgroup) run on the CUs the reprojection and the
+// single-workgroup plan leave idle, instead of as their own launch before.
+// The insertion writes pyramid slots only, which nothing else in the launch
+// reads; outputs are bit-identical to the two separate launches.
+struct InsArgs {
+  const void* src;
+  InsLevels lv;
+  int L, C, H, W, gx, gy, ntile;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(kPT) reproject_plan_insert_kernel(RArgs R, Plan plan, InsArgs I,
+                                                                    int nrep) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int b = blockIdx.x;
+  if (b == 0) {
+    plan_block(R.ii, R.jj, R.kk, R.E, R.num_patches, R.num_poses, R.t0, R.N, plan, lds);
+    return;
+  }
+  if (b == 1) {
+    edge_order_block(R.jj, R.E, R.N2, R.order, reinterpret_cast<int*>(lds));
+    return;
+  }
+  if (b < 2 + nrep) {
+    const int PP = R.P * R.P;
+    const int t = (b - 2) * kPT + threadIdx.x;
+    if (t >= R.E * PP) return;
+    reproject_pixel(R.poses, R.patches, R.intrinsics, R.ii, R.jj, R.kk, t / PP, t % PP, R.P,
+                    R.num_poses, R.num_patches, R.coords);
+    return;
+  }
+  static_assert(kPT == 512, "two 256-thread insertion tiles per workgroup");
+  const int half = threadIdx.x >> 8, t = 2 * (b - 2 - nrep) + half;
+  const bool act = t < I.ntile;
+  const int tt = act ? t : 0;
+  float* tile = reinterpret_cast<float*>(lds) + half * kInsTC * kInsCS;
+  ins_tile<T>(static_cast<const T*>(I.src), I.lv, I.L, I.C, I.H, I.W, tt % I.gx,
+              (tt / I.gx) % I.gy, tt / (I.gx * I.gy), threadIdx.x & 255, act, tile);
 }
 
 // ===========================================================================
@@ -1227,6 +1270,10 @@ static void set_attrs() {
                               hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
     (void)hipFuncSetAttribute((const void*)reproject_plan_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
+    (void)hipFuncSetAttribute((const void*)reproject_plan_insert_kernel<float>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
+    (void)hipFuncSetAttribute((const void*)reproject_plan_insert_kernel<__half>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
     attr = true;
   }
 }
@@ -1273,6 +1320,59 @@ int ba_window_reproject_plan(const float* poses, const float* patches, const flo
   const int total = E * P * P;
   hipLaunchKernelGGL(reproject_plan_kernel, dim3(2 + (total + kPT - 1) / kPT), dim3(kPT), kWLds,
                      as_stream(stream), r, plan);
+  return launch_status();
+}
+
+// reproject + order + plan + frame insertion (src [C, H, W] NCHW fp32 / fp16,
+// dst[l] the channels-last slot of level l, scale[l] in {1, 2, 4, 8})
+int ba_window_reproject_plan_insert(const float* poses, const float* patches,
+                                    const float* intrinsics, const int64_t* ii, const int64_t* jj,
+                                    const int64_t* kk, int E, int P, int num_poses,
+                                    int num_patches, int N2, float* coords, int* order, int t0,
+                                    int t1, char* scratch, int* status, const void* src,
+                                    void* const* dst, const int* scale, int L, int C, int H, int W,
+                                    int half, void* stream) {
+  set_attrs();
+  Plan plan = plan_view(scratch, E, status);
+  plan.t0d = nullptr;
+  RArgs r;
+  r.poses = poses;
+  r.patches = patches;
+  r.intrinsics = intrinsics;
+  r.ii = ii;
+  r.jj = jj;
+  r.kk = kk;
+  r.E = E;
+  r.P = P;
+  r.num_poses = num_poses;
+  r.num_patches = num_patches;
+  r.N2 = N2;
+  r.t0 = t0;
+  r.N = t1 - t0;
+  r.coords = coords;
+  r.order = order;
+  InsArgs I = {};
+  I.src = src;
+  I.L = L;
+  I.C = C;
+  I.H = H;
+  I.W = W;
+  I.lv.mem = 1;
+  for (int l = 0; l < L; l++) {
+    I.lv.dst[l] = dst[l];
+    I.lv.s[l] = scale[l];
+  }
+  I.gx = (W + kInsTX - 1) / kInsTX;
+  I.gy = (H + kInsTY - 1) / kInsTY;
+  I.ntile = I.gx * I.gy * ((C + kInsTC - 1) / kInsTC);
+  const int nrep = (E * P * P + kPT - 1) / kPT;
+  const dim3 grid(2 + nrep + (I.ntile + 1) / 2);
+  if (half)
+    hipLaunchKernelGGL(reproject_plan_insert_kernel<__half>, grid, dim3(kPT), kWLds,
+                       as_stream(stream), r, plan, I, nrep);
+  else
+    hipLaunchKernelGGL(reproject_plan_insert_kernel<float>, grid, dim3(kPT), kWLds,
+                       as_stream(stream), r, plan, I, nrep);
   return launch_status();
 }
 

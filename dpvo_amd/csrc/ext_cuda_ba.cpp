@@ -351,6 +351,58 @@ std::vector<torch::Tensor> ba_reproject_ordered_plan(torch::Tensor poses, torch:
   return {coords.view({1, E, 2, P, P}), order, ws};
 }
 
+// ... plus the new frame's pyramid insertion in the same launch (src [C, H, W]
+// NCHW, dst[l] the channels-last [C, H/s, W/s] slot view of level l)
+std::vector<torch::Tensor> ba_reproject_ordered_plan_insert(
+    torch::Tensor poses, torch::Tensor patches, torch::Tensor intrinsics, torch::Tensor ii,
+    torch::Tensor jj, torch::Tensor kk, int N2, int t0, int t1, torch::Tensor src,
+    std::vector<torch::Tensor> dst, std::vector<int64_t> scales) {
+  poses = f32_contig(poses, "poses");
+  patches = f32_contig(patches, "patches");
+  intrinsics = f32_contig(intrinsics, "intrinsics");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  ii = idx64(ii, "ii");
+  jj = idx64(jj, "jj");
+  kk = idx64(kk, "kk");
+  check_device(src, "src");
+  TORCH_CHECK(src.dim() == 3, "src must be [C, H, W]");
+  TORCH_CHECK(src.scalar_type() == torch::kFloat32 || src.scalar_type() == torch::kFloat16,
+              "src must be float32 or float16");
+  TORCH_CHECK(dst.size() == scales.size() && !dst.empty(), "one scale per destination level");
+  src = src.contiguous();
+  const int C = src.size(0), H = src.size(1), W = src.size(2);
+  std::vector<void*> ptrs;
+  std::vector<int> sc;
+  for (size_t l = 0; l < dst.size(); l++) {
+    const torch::Tensor& d = dst[l];
+    check_device(d, "dst");
+    const int s = (int)scales[l];
+    TORCH_CHECK(d.scalar_type() == src.scalar_type() && d.dim() == 3 && d.size(0) == C && s > 0 &&
+                    d.size(1) == H / s && d.size(2) == W / s,
+                "dst level ", l, " must be [C, H/s, W/s] of src's dtype");
+    TORCH_CHECK(d.stride(0) == 1 && d.stride(2) == C && d.stride(1) == (int64_t)C * d.size(2),
+                "dst level ", l, " must be channels-last");
+    ptrs.push_back(d.data_ptr());
+    sc.push_back(s);
+  }
+  const int P = patches.size(-1);
+  const int E = ii.numel();
+  TORCH_CHECK(jj.numel() == E && kk.numel() == E, "ii, jj, kk must have equal length");
+  auto coords = torch::empty({E, 2, P, P}, poses.options());
+  auto order = torch::empty({E}, poses.options().dtype(torch::kInt32));
+  const size_t wsb = dpvo_ba_workspace_bytes(E, t0, t1);
+  auto ws = torch::empty({(int64_t)wsb}, poses.options().dtype(torch::kUInt8));
+  check_status(dpvo_reproject_ordered_plan_insert(
+                   poses.data_ptr<float>(), patches.data_ptr<float>(), intrinsics.data_ptr<float>(),
+                   ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), kk.data_ptr<int64_t>(), E, P,
+                   poses.numel() / 7, patches.numel() / (3 * P * P), N2, coords.data_ptr<float>(),
+                   order.data_ptr<int32_t>(), t0, t1, ws.data_ptr(), wsb, src.data_ptr(),
+                   ptrs.data(), sc.data(), (int)ptrs.size(), C, H, W, dtype_code(src),
+                   current_stream()),
+               "cuda_ba.reproject_ordered_plan_insert");
+  return {coords.view({1, E, 2, P, P}), order, ws};
+}
+
 // Device-t0 variants (graph-replayed DPVO updates: the window start moves
 // every frame while shapes stay fixed): t0_dev is an int32 device scalar, N =
 // t1 - t0 the (fixed) number of free poses.
@@ -923,6 +975,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("delta_tstamps") = py::none(), py::arg("delta_count") = py::none());
   m.def("edges_loop", &edges_loop, "PatchGraph.edges_loop (patchgraph.py:65-91), device count");
   m.def("edges_loop_work_floats", []() { return (int64_t)dpvo_edges_loop_work_floats(); });
+  m.def("reproject_ordered_plan_insert", &ba_reproject_ordered_plan_insert,
+        "reproject + edge order + BA plan + the new frame's pyramid insertion, one launch");
   m.def("reproject_ordered", &ba_reproject_ordered,
         "reproject + edge order by target frame (for cuda_corr.forward_levels(order=))");
   m.def("select_path", [](int mode) { check_status(dpvo_ba_select_path(mode), "select_path"); },

@@ -75,7 +75,7 @@ def neighbors(ii, jj):
     return cuda_ba.neighbors(ii, jj)
 
 
-def reproject(poses, patches, intrinsics, ii, jj, kk, mem=None, plan_window=None):
+def reproject(poses, patches, intrinsics, ii, jj, kk, mem=None, plan_window=None, insert=None):
     """cuda_ba.reproject (ba_cuda.cu:379-429, 585-616).  With ``mem`` (the
     feature ring size the targets jj index), also returns the A-CORR edge
     order (int32 [E], edges grouped by target frame) computed in the same
@@ -83,7 +83,20 @@ def reproject(poses, patches, intrinsics, ii, jj, kk, mem=None, plan_window=None
     ``plan_window=(t0, t1)`` the same launch also groups the edges for the
     update's BA: ``coords, order, ws = reproject(..., mem=36, plan_window=(t0, t1))``
     and later ``BA(..., plan=ws)`` (identical to :func:`plan`; the window path
-    must cover the shape, see :func:`plan`)."""
+    must cover the shape, see :func:`plan`).  With ``insert=(fmap, dst, scales)``
+    (and mem, plan_window) the same launch also inserts the update's new frame
+    into the channels-last pyramid (``altcorr.insert_frame``'s work; ``dst``
+    are the per-level slot views), bit-identical to the separate launches."""
+    if insert is not None:
+        # insert = (fmap [C, H, W], [channels-last slot view per level], scales):
+        # the new frame's pyramid insertion (altcorr.insert_frame) in the same launch
+        if mem is None or plan_window is None:
+            raise ValueError("reproject: insert needs mem and plan_window")
+        fmap, dst, scales = insert
+        t0, t1 = plan_window
+        return tuple(cuda_ba.reproject_ordered_plan_insert(
+            poses, patches, intrinsics, ii, jj, kk, int(mem), int(t0), int(t1), fmap, list(dst),
+            [int(s) for s in scales]))
     if mem is None:
         if plan_window is not None:
             raise ValueError("reproject: plan_window needs mem")

@@ -333,6 +333,21 @@ int dpvo_reproject_ordered_plan(const float* poses, const float* patches,
                                 const int64_t* kk, int E, int P, int num_poses, int num_patches,
                                 int N2, float* coords, int32_t* order, int t0, int t1,
                                 void* workspace, size_t workspace_bytes, void* stream);
+/* dpvo_reproject_ordered_plan plus, in the same launch, the insertion of the
+   update's new frame into the channels-last pyramid (dpvo_feature_pyramid_insert's
+   arguments: src [C, H, W] NCHW level-1 frame, dst[l] the channels-last slot of
+   level l, scale[l] in {1, 2, 4, 8}, dtype F32 / F16).  The insertion tiles run
+   on the CUs the reprojection and the single-workgroup plan leave idle (DPVO
+   inserts the frame in __call__ just before update(); nothing in this launch
+   reads the slot it writes).  Outputs bit-identical to the separate calls. */
+int dpvo_reproject_ordered_plan_insert(const float* poses, const float* patches,
+                                       const float* intrinsics, const int64_t* ii,
+                                       const int64_t* jj, const int64_t* kk, int E, int P,
+                                       int num_poses, int num_patches, int N2, float* coords,
+                                       int32_t* order, int t0, int t1, void* workspace,
+                                       size_t workspace_bytes, const void* src, void* const* dst,
+                                       const int* scale, int L, int C, int H, int W, int dtype,
+                                       void* stream);
 /* Device-scalar variants for graph-replayed DPVO updates (the window start t0
    moves every frame, shapes stay fixed): t0 is read from the int32 device
    scalar *t0_dev, N = t1 - t0 is given.  Same results as the host-t0 calls. */

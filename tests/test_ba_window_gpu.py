@@ -256,3 +256,41 @@ def test_plan_grouping_matches_host(cb, gpu, E, nk, M, seed):
     np.testing.assert_array_equal(epos, ref[0])
     np.testing.assert_array_equal(pkk, ref[3])
     np.testing.assert_array_equal(pmask, ref[2])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_reproject_plan_insert_fused_is_bit_identical(cb, gpu, dtype):
+    """reproject(mem=, plan_window=, insert=) (dpvo_reproject_ordered_plan_insert:
+    the new frame's pyramid insertion in the reprojection + plan launch) ==
+    reproject(mem=, plan_window=) + altcorr.insert_frame: coords, order,
+    the plan (BA(plan=ws) bits) and every written pyramid slot."""
+    from dpvo_amd import altcorr, fastba
+
+    G = synthetic.make_config("cfg2", seed=12)
+    D = G.to(gpu)
+    t0, t1, mem, levels = 1, G.F, 16, (1, 2, 4, 8)
+    pyr_nchw = synthetic.make_features(mem=mem, C=128, levels=levels, seed=3, device=gpu,
+                                       dtype=dtype)
+    pa = [synthetic.channels_last(p).clone() for p in pyr_nchw]
+    pb = [synthetic.channels_last(p).clone() for p in pyr_nchw]
+    src = torch.randn(128, pyr_nchw[0].shape[3], pyr_nchw[0].shape[4], device=gpu).to(dtype)
+    slot = 5
+    c_ref, o_ref, ws_ref = fastba.reproject(D.poses, D.patches, D.intrinsics, D.ii, D.jj, D.kk,
+                                            mem=mem, plan_window=(t0, t1))
+    altcorr.insert_frame(src, pa, slot, levels)
+    c, o, ws = fastba.reproject(D.poses, D.patches, D.intrinsics, D.ii, D.jj, D.kk, mem=mem,
+                                plan_window=(t0, t1),
+                                insert=(src, [p[0, slot] for p in pb], levels))
+    torch.cuda.synchronize()
+    assert torch.equal(c, c_ref) and torch.equal(o, o_ref)
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
+    lm = torch.tensor([1e-4], device=gpu)
+    outs = []
+    for w in (ws_ref, ws):
+        poses, patches = D.poses.clone(), D.patches.clone()
+        fastba.BA(poses, patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj, D.kk, t0, t1,
+                  M=G.M, iterations=2, plan=w)
+        outs.append((poses, patches))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert cb.check_status(D.poses) == 0
