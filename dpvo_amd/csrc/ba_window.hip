@@ -31,6 +31,9 @@
 //   * Grid <= 256 workgroups (one per CU, all co-resident); flags are
 //     epoch-tagged (graph-replayable) and every spin-wait has a wall-clock
 //     timeout (status bit 16) so the grid always drains.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 
@@ -129,24 +132,39 @@ __device__ __forceinline__ void wg_block(const WArgs& A, int g, int& a, int& b, 
 // ===========================================================================
 // plan: group edges by patch (one workgroup, 512 threads)
 // ===========================================================================
+// per-edge capacity of a plan sized for E edges, and its LDS bytes
+__host__ __device__ constexpr int plan_cap(int E) { return (E + 15) & ~15; }
+// U: hd + mask (8 cap B) or the bitonic keys (u64 up to 8192 entries, u32 above)
+__host__ __device__ constexpr size_t plan_u_bytes(int cap) {
+  size_t p2 = 1;
+  while (p2 < (size_t)cap) p2 <<= 1;
+  const size_t keys = p2 <= 8192 ? 8 * p2 : 4 * p2;
+  return keys > 8 * (size_t)cap ? keys : 8 * (size_t)cap;
+}
+__host__ __device__ constexpr size_t plan_lds_bytes(int cap) {
+  return 256 + 6 * (size_t)cap + (((size_t)cap + 15) & ~(size_t)15) + plan_u_bytes(cap);
+}
+static_assert(plan_lds_bytes(kWMaxE) <= (size_t)kWLds, "plan LDS");
+
 __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
                                            const int64_t* __restrict__ jj,
                                            const int64_t* __restrict__ kk, int E, int num_patches,
                                            int num_poses, int t0, int N, const Plan& plan,
-                                           char* lds) {
+                                           char* lds, int cap = kWMaxE) {
   if (plan.t0d) t0 = *plan.t0d;
-  // LDS (153.9 KB at kWMaxE = 10240): per-edge arrays as u16 / u8, one union
-  //   [ctl 256 B | code u16[E] | key u16[E] -> ranked | spos u16[E] | head u8[E] | U 80 KB]
-  //   U: counting sort hist int[kHistMax], later hd int[E] + mask u32[E];
+  // LDS (plan_lds_bytes(cap), cap >= E; 153.9 KB at kWMaxE = 10240): per-edge
+  // arrays as u16 / u8, one union
+  //   [ctl 256 B | code u16[cap] | key u16[cap] -> ranked | spos u16[cap] | head u8[cap] | U]
+  //   U (>= 16 cap B): counting sort hist int[R], later hd int[E] + mask u32[E];
   //      bitonic sort keys (u64 for E <= 8192, u32 (key << 14 | e) above)
   const int tid = threadIdx.x, lane = tid & 63, T = kPT;
   int* ctl = (int*)lds;                  // [64]
   int* scr = ctl + 16;                   // scan scratch [>= 17]
   unsigned short* code = (unsigned short*)(lds + 256);           // ci | cj << 8 (5 bits each)
-  unsigned short* key = code + kWMaxE;                           // kk - kmin, later ranked edges
-  unsigned short* spos = key + kWMaxE;                           // edge at position p
-  unsigned char* head = (unsigned char*)(spos + kWMaxE);         // head flags
-  char* U = (char*)head + al16(kWMaxE);
+  unsigned short* key = code + cap;                              // kk - kmin, later ranked edges
+  unsigned short* spos = key + cap;                              // edge at position p
+  unsigned char* head = (unsigned char*)(spos + cap);            // head flags
+  char* U = (char*)head + al16(cap);
   const int kmaxc = num_patches - 1;
   if (tid == 0) {
     ctl[0] = 0x7fffffff;  // kmin
@@ -208,7 +226,7 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
   kmin = ctl[0];
   const int R = ctl[1] - kmin + 1;
   unsigned short* pos_edge = spos;  // the sorted order, wherever it ends up
-  if (R <= kHistMax) {
+  if (R <= kHistMax && (size_t)R * 4 <= plan_u_bytes(cap)) {
     int* hist = (int*)U;  // [R]
     for (int v = tid; v < R; v += T) hist[v] = 0;
     for (int p = tid; p < E; p += T) head[p] = 0;
@@ -335,7 +353,7 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
   }
   if (tid == 0) plan.poff[nuniq] = E;
   // free-pose masks: OR over the patch's edges (positions are contiguous)
-  unsigned* mask = (unsigned*)(U + sizeof(int) * kWMaxE);  // [nuniq]
+  unsigned* mask = (unsigned*)(U + sizeof(int) * cap);  // [nuniq]
   for (int u = tid; u < nuniq; u += T) mask[u] = 0u;
   __syncthreads();
   for (int p = tid; p < E; p += T) {
@@ -417,7 +435,8 @@ __global__ void __launch_bounds__(kPT) reproject_plan_insert_kernel(RArgs R, Pla
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int b = blockIdx.x;
   if (b == 0) {
-    plan_block(R.ii, R.jj, R.kk, R.E, R.num_patches, R.num_poses, R.t0, R.N, plan, lds);
+    plan_block(R.ii, R.jj, R.kk, R.E, R.num_patches, R.num_poses, R.t0, R.N, plan, lds,
+               plan_cap(R.E));
     return;
   }
   if (b == 1) {
@@ -1150,6 +1169,15 @@ static WGrid window_grid(int E, int N) {
   // every block alike, so large windows split all blocks evenly
   w.So = E > 2048 ? 4 : 1;
   w.Sd = 4;
+  // tuning override (instrumentation): DPVO_BA_SHARES="Sd,So"
+  static const char* ov = getenv("DPVO_BA_SHARES");
+  if (ov) {
+    int sd = 0, so = 0;
+    if (sscanf(ov, "%d,%d", &sd, &so) == 2 && sd >= 1 && so >= 1 && sd <= 16 && so <= 16) {
+      w.Sd = sd;
+      w.So = so;
+    }
+  }
   auto G = [&]() { return N * w.Sd + (w.NB - N) * w.So; };
   while (G() > kWMaxG && w.Sd > 1) {
     if (w.Sd > w.So) w.Sd--;
@@ -1367,11 +1395,16 @@ int ba_window_reproject_plan_insert(const float* poses, const float* patches,
   I.ntile = I.gx * I.gy * ((C + kInsTC - 1) / kInsTC);
   const int nrep = (E * P * P + kPT - 1) / kPT;
   const dim3 grid(2 + nrep + (I.ntile + 1) / 2);
+  // LDS sized for this E (the plan's need), not the kWMaxE maximum: the
+  // insertion tiles then run several workgroups per CU beside the plan
+  size_t lds = plan_lds_bytes(plan_cap(E));
+  lds = std::max(lds, sizeof(float) * 2 * kInsTC * kInsCS);
+  lds = std::max(lds, sizeof(int) * (size_t)(kOrderBins + 2));
   if (half)
-    hipLaunchKernelGGL(reproject_plan_insert_kernel<__half>, grid, dim3(kPT), kWLds,
+    hipLaunchKernelGGL(reproject_plan_insert_kernel<__half>, grid, dim3(kPT), lds,
                        as_stream(stream), r, plan, I, nrep);
   else
-    hipLaunchKernelGGL(reproject_plan_insert_kernel<float>, grid, dim3(kPT), kWLds,
+    hipLaunchKernelGGL(reproject_plan_insert_kernel<float>, grid, dim3(kPT), lds,
                        as_stream(stream), r, plan, I, nrep);
   return launch_status();
 }
