@@ -168,3 +168,28 @@ def test_cfg4_full_size_runs_and_agrees_with_sharded(cb, gpu):
                      t0, t1)
         tot += cb.gba_packed(w2, G.E, t0, t1, nblk)
     torch.testing.assert_close(tot, full, rtol=1e-9, atol=1e-8)
+
+
+def test_cfg4_full_size_matches_oracle(cb, gpu):
+    """BASELINE cfg4 at full size (1024 x 96, 131k edges, N = 1023 free poses),
+    one iteration, against the oracle's result (dense fp64 S + Cholesky,
+    72 s on one CPU core: computed once by oracle/make_cfg4_reference.py and
+    committed as tests/golden/cfg4_ba1.npz with a digest of its inputs, which
+    this test rebuilds from the same seed).  Tolerances of the cfg4s/cfg4m
+    tests (poses 2e-5 abs, inverse depths 1e-4 rel + 1e-5)."""
+    import hashlib
+
+    from conftest import golden
+
+    g = golden("cfg4_ba1")
+    G = synthetic.make_config("cfg4", seed=0)
+    h = hashlib.sha256()
+    for a in (G.poses, G.patches, G.intrinsics, G.ii, G.jj, G.kk, G.target, G.weight):
+        h.update(np.ascontiguousarray(a.numpy()).tobytes())
+    assert h.hexdigest() == str(g["digest"]), "cfg4 inputs differ from the fixture's"
+    P, K = _gpu(cb, G, gpu, int(g["t0"]), int(g["t1"]), 1)
+    assert cb.check_status(torch.zeros(1, device=gpu)) == 0
+    np.testing.assert_allclose(P, g["poses"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(K[:, 2, 1, 1], g["depth"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(K[:, 2, 0, 0], g["depth00"], rtol=1e-4, atol=1e-5)
+    assert np.abs(P - G.poses.numpy()).max() > 1e-4  # the step is not trivially zero
