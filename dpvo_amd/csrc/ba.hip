@@ -43,7 +43,7 @@ constexpr int kMaxFree = 20;  // pose-block masks are 32-bit; lower S blocks of 
 constexpr int kPerThread = kMaxSetupE / kSetupThreads;
 constexpr int kCtlBytes = 512;
 constexpr int kSetupLds = 160 * 1024;
-constexpr int kMarks = 128;
+constexpr int kMarks = 1152;  // [0, 128) phases; window kernel: [128 + 256 it + g] assembled, [640 + 256 it + g] all partials seen
 constexpr int kNoPose = 31;
 constexpr int kEC = 16;  // doubles per position record of E terms
 

@@ -253,8 +253,9 @@ void ba_forward_planned(torch::Tensor ws, torch::Tensor poses, torch::Tensor pat
   track_status(ws, poses, E, t0, t1);
 }
 
-// Same call; returns the 128 phase marks followed by the per-workgroup marks (100 MHz ticks:
-// start, setup, then linearize/patch/schur/solve/update per iteration).
+// Same call; returns the 1152 phase marks (100 MHz ticks: [0, 128) phases; window kernel
+// [128 + 256 it + g] / [640 + 256 it + g] per-workgroup assembled / partials seen) followed by
+// the multi-kernel path's per-workgroup marks.
 torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
                                torch::Tensor intrinsics, torch::Tensor target, torch::Tensor weight,
                                torch::Tensor lmbda, torch::Tensor ii, torch::Tensor jj,
@@ -262,7 +263,7 @@ torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
                                bool eff_impl) {
   auto ws = ba_forward_ws(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, PPF, t0,
                           t1, iterations, eff_impl);
-  auto out = torch::zeros({128}, poses.options().dtype(torch::kInt64));
+  auto out = torch::zeros({1152}, poses.options().dtype(torch::kInt64));
   if (!ws.defined()) return out;
   check_status(dpvo_ba_phase_marks(ws.data_ptr(), ii.numel(), t0, t1, out.data_ptr<int64_t>(),
                                    current_stream()),

@@ -58,3 +58,17 @@ print(f"{arg}: E={G.E} N={t1 - t0} iterations={iters}")
 for k, v in acc.items():
     v = sorted(v)
     print(f"{k:34s} median {v[len(v) // 2]:8.2f} us")
+
+# per-workgroup spread (window kernel stamps [128 + 256 it + g] assembled,
+# [640 + 256 it + g] every partial seen), last call
+if m[128] and len(m) >= 1152:
+    import statistics
+
+    G = sum(1 for g in range(256) if m[128 + g])
+    for it in range(min(iters, 2)):
+        asm = [(m[128 + 256 * it + g] - m[0]) * 0.01 for g in range(G)]
+        seen = [(m[640 + 256 * it + g] - m[0]) * 0.01 for g in range(G)]
+        order = sorted(range(G), key=lambda g: asm[g])
+        print(f"it{it}: {G} workgroups assembled at {min(asm):.2f}..{max(asm):.2f} us "
+              f"(median {statistics.median(asm):.2f}); all partials seen at "
+              f"{min(seen):.2f}..{max(seen):.2f} us; slowest workgroups {order[-5:]}")
