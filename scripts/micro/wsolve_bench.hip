@@ -124,9 +124,9 @@ int main(int argc, char** argv) {
   hipMemcpy(h, dst, sizeof(h), hipMemcpyDeviceToHost);
   printf("pre %lld piv0 %lld |", h[1] - h[0], 0LL);
   for (int k = 0; k < N; k++) printf(" %lld", h[2 + k] - (k ? h[1 + k] : h[1]));
-  printf(" | solve %lld", h[41] - h[40]);
-  printf(" | k2: w0 col %lld chol %lld panel %lld ; w1 done %lld (from step start)", h[50] - h[3],
-         h[51] - h[50], h[52] - h[51], h[53] - h[3]);
+  printf(" | post %lld | solve %lld", h[40] - h[1 + N], h[41] - h[40]);
+  printf(" | k2 (from step start): w0 %lld w1 %lld w2 %lld w3 %lld w3+ldl %lld", h[50] - h[3],
+         h[52] - h[3], h[53] - h[3], h[54] - h[3], h[55] - h[3]);
   for (int it = 0; it < refine; it++) printf(" ref%d %lld", it, h[42 + it] - (it ? h[41 + it] : h[41]));
   printf("\n");
   std::vector<double> got(n);
