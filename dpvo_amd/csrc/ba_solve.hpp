@@ -125,24 +125,6 @@ __device__ __forceinline__ void fwd6(const float L[6][6], const float ri[6], con
   }
 }
 
-// lanes 0..20 write the 21 lower entries of a register-resident factor
-// (1/L_qq on the diagonal).  Fully unrolled selects: indexing the register
-// arrays with a lane-dependent index would put them in scratch memory.
-__device__ __forceinline__ void store_piv(float* pv, const float L[6][6], const float ri[6],
-                                          int lane) {
-  float v = 0.0f;
-  int off = 0;
-#pragma unroll
-  for (int r = 0, idx = 0; r < 6; r++)
-#pragma unroll
-    for (int c = 0; c <= r; c++, idx++)
-      if (lane == idx) {
-        v = (r == c) ? ri[r] : L[r][c];
-        off = 6 * r + c;
-      }
-  if (lane < 21) pv[off] = v;
-}
-
 // lanes 0-5 store column `lane` of Linv = L^-1 of a register-resident pivot
 // factor into a row-major 6x6 block (zeros above the diagonal included)
 __device__ __forceinline__ void store_linv(float* out, const float L[6][6], const float ri[6],
@@ -211,6 +193,18 @@ __device__ __forceinline__ void residual64(const double* S, const double* y, con
   if (row < n && part == 0) v[row] = (float)(y[row] - s);
 }
 
+#ifdef WSOLVE_STEP_STAMPS
+#define WSTAMP_DBG(slot)                                                        \
+  do {                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+    if (st && k == 2 && lane == 0) st[slot] = (long long)__builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+  } while (0)
+#else
+#define WSTAMP_DBG(slot) \
+  do {                   \
+  } while (0)
+#endif
 __device__ __forceinline__ void wstamp(long long* st, int slot) {
   if (st && threadIdx.x == 0) st[slot] = (long long)__builtin_amdgcn_s_memtime();
 }
@@ -419,7 +413,6 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
   if (wid == 0) {  // pivot 0 and panel column 0
     float L[6][6], ri[6];
     const bool ok = chol6_reg(s.A, L, ri);
-    store_piv(s.A, L, ri, lane);
     store_linv(s.Z, L, ri, lane);
     if (!ok && lane == 0) *fail = 1;
     for (int t = lane; t < 6 * (N - 1); t += 64) {
@@ -463,15 +456,26 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
 #pragma unroll
             for (int q = 0; q < 6; q++) v1[z] -= a[q] * B[6 * z + q];
         }
+        WSTAMP_DBG(56);
+        // pivot rows (lanes 0-5) to every lane through LDS: the rows go to the
+        // pivot block (only Linv is kept of it; D^-1 overwrites it later)
+        float* pv = s.A + 36 * lblk(c1, c1);
+        if (lane < 6) st_row(pv + 6 * lane, v0);
+        wave_lds_sync();
         float m[6][6], L[6][6], ri[6];
+        {
+          float P[36];
+          ld_blk(pv, P);
 #pragma unroll
-        for (int r = 0; r < 6; r++)
+          for (int r = 0; r < 6; r++)
 #pragma unroll
-          for (int c = 0; c <= r; c++)
-            m[r][c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v0[c]), r));
+            for (int c = 0; c <= r; c++) m[r][c] = P[6 * r + c];
+        }
+        WSTAMP_DBG(57);
         const bool ok = chol6_m(m, L, ri);
-        store_piv(s.A + 36 * lblk(c1, c1), L, ri, lane);
+        WSTAMP_DBG(58);
         store_linv(s.Z + 36 * lblk(c1, c1), L, ri, lane);
+        WSTAMP_DBG(59);
         if (!ok && lane == 0) *fail = 1;
         if (lane >= 6 && lane < nr) {
           float lv[6];

@@ -127,6 +127,10 @@ int main(int argc, char** argv) {
   printf(" | post %lld | solve %lld", h[40] - h[1 + N], h[41] - h[40]);
   printf(" | k2 (from step start): w0 %lld w1 %lld w2 %lld w3 %lld w3+ldl %lld", h[50] - h[3],
          h[52] - h[3], h[53] - h[3], h[54] - h[3], h[55] - h[3]);
+#ifdef WSOLVE_STEP_STAMPS
+  printf(" | w0: update %lld readlane %lld chol %lld stores %lld panel %lld", h[56] - h[3],
+         h[57] - h[56], h[58] - h[57], h[59] - h[58], h[50] - h[59]);
+#endif
   for (int it = 0; it < refine; it++) printf(" ref%d %lld", it, h[42 + it] - (it ? h[41 + it] : h[41]));
   printf("\n");
   std::vector<double> got(n);
