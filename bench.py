@@ -132,7 +132,8 @@ def sharded_main(args, torch, dist, world, rank, local, dev):
         torch.cuda.synchronize()
         for k in range(3):
             acc[k] += ev[k].elapsed_time(ev[k + 1]) / reps
-    status = sb.backend.status(st)[0]
+    info = sb.backend.status(st)
+    status = info[0]
     if world > 1:
         t = torch.tensor([elapsed] + acc, device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -159,6 +160,8 @@ def sharded_main(args, torch, dist, world, rank, local, dev):
             "all_reduce_bytes": sb.allreduce_bytes,
             "all_reduce_share": acc[1] / it_ms if it_ms > 0 else 0.0,
             "ba_status": status,
+            "structure": dict(zip(["status", "patches", "items", "blocks", "interior", "border",
+                                   "g", "superblocks"], info)),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

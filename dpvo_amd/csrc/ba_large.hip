@@ -58,8 +58,8 @@ constexpr int kMaxNB6 = 6 * kMaxBorder;
 constexpr int kMaxN = 8192;
 constexpr int kItemsPerEdge = 25;  // max over k of min(k (2k+1), kMaxSet (kMaxSet+1) / 2) / k
 constexpr int kT = 256;
-constexpr int kPanel = 32;      // columns per LDS panel in the superblock products
 constexpr int kMetaInts = 16;
+constexpr int kBP = 32;        // border Schur partial groups
 
 // status bits (Meta::status)
 constexpr int kStChol = 1;      // a pivot was not positive: dX = 0 this iteration
@@ -94,6 +94,7 @@ struct Ws {
   double *D, *Lo0, *Lo1, *Y1, *Y2;  // superblock storage [SB2]
   double *R, *BT;                   // [SBR] rhs / solution, border columns
   double *Cb, *rb, *dXB;            // border system
+  double* Pb;                       // [kBP][6 nB][1 + 6 nB] border Schur partials
   double* dX;                       // [6N]
   void* tmp;                        // rocPRIM temporary storage
   size_t tmp_bytes;
@@ -181,6 +182,7 @@ static size_t layout(int E, int N, char* base, Ws* w) {
   t.Cb = (double*)take(8 * (size_t)kMaxNB6 * kMaxNB6);
   t.rb = (double*)take(8 * (size_t)kMaxNB6);
   t.dXB = (double*)take(8 * (size_t)kMaxNB6);
+  t.Pb = (double*)take(8 * (size_t)kBP * kMaxNB6 * (kMaxNB6 + 1));
   t.dX = (double*)take(8 * 6 * (size_t)Np);
   t.tmp_bytes = rocprim_tmp_bytes(E);
   t.tmp = take(t.tmp_bytes);
@@ -692,76 +694,236 @@ __device__ bool wg_gj_inverse(double* A, int n, int lda, double* colk, double* r
   return bad == 0;
 }
 
-// dst[m x ncols] = Dinv[m x m] (LDS) * op(src) where op(src) = src (m x ncols,
-// row stride lds_) or src^T (src stored ncols x m, row stride lds_).  dst may
-// alias src (panels are staged through LDS first).
-__device__ void wg_lmul(const double* Dinv, int m, const double* src, int lds_, bool trans,
-                        int ncols, double* dst, int ldd, double* panel) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  for (int c0 = 0; c0 < ncols; c0 += kPanel) {
-    const int nc = min(kPanel, ncols - c0);
-    __syncthreads();
-    for (int q = tid; q < m * kPanel; q += nt) {
-      const int r = q / kPanel, c = q % kPanel;
-      double v = 0.0;
-      if (c < nc) v = trans ? src[(size_t)(c0 + c) * lds_ + r] : src[(size_t)r * lds_ + c0 + c];
-      panel[q] = v;
+// Superblock kernels.  Each level of the reduction is a few launches whose
+// workgroups do ONE round trip to HBM each: every operand a workgroup needs
+// (an m x m factor, a 32-column panel) is loaded into LDS at once, then the
+// work runs from LDS and registers.  kMaxM <= 96.
+//   k_cr_inv   one 1024-thread workgroup per eliminated superblock: D^-1 in
+//              place (register Gauss-Jordan, 32 x 32 threads x 3 x 3 entries)
+//   k_cr_mul   (superblock, 32-column panel): Y1 = D^-1 A[o,l], Y2 = D^-1 A[o,r],
+//              Z = D^-1 R_o
+//   k_cr_b     (kept superblock, panel): Schur updates of D_e, R_e and the new
+//              coupling
+//   k_cr_back  (eliminated superblock, panel): x_o = Z_o - Y1 x_l - Y2 x_r
+constexpr int kTB = 1024;
+constexpr int kPW = 32;                        // panel width (columns)
+constexpr int kPanelsM = (kMaxM + kPW - 1) / kPW;
+constexpr int kPanelsR = (1 + kMaxNB6 + kPW - 1) / kPW;
+static_assert(kMaxM <= 96, "register Gauss-Jordan tiles 96 x 96");
+
+__device__ __forceinline__ double rcp_f64(double p) {
+  double r = __builtin_amdgcn_rcp(p);  // ~2^-26, then two Newton steps
+  double e = fma(-p, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-p, r, 1.0);
+  return fma(r, e, r);
+}
+
+// Gauss-Jordan inverse (no pivoting; SPD) of the n x n matrix src (row stride
+// lda) into dst (row stride n; global or LDS; may alias src: every load
+// happens before the first barrier).  1024 threads; thread (ty, tx) owns
+// entries (ty + 32 p, tx + 32 q).  Per pivot k ONE barrier: the owners of row
+// k (one half-wave) take the pivot by a lane shuffle, publish the scaled row
+// a_kj / a_kk and 1 / a_kk, the owners of column k publish it (parity
+// double-buffered LDS: a writer of step k + 2 has passed the barrier of step
+// k + 1, so every reader of step k is done); every entry is then one FMA.
+__device__ bool wg_gj_inverse_reg(const double* src, int n, int lda, double* dst, double* vbuf) {
+  __shared__ int bad;
+  const int tid = threadIdx.x, ty = tid >> 5, tx = tid & 31;
+  double a[3][3];
+#pragma unroll
+  for (int p = 0; p < 3; p++)
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const int i = ty + 32 * p, j = tx + 32 * q;
+      a[p][q] = (i < n && j < n) ? src[(size_t)i * lda + j] : 0.0;
+    }
+  if (tid == 0) bad = 0;
+  constexpr int kV = 2 * kMaxM + 2;
+  for (int k = 0; k < n; k++) {
+    double* colk = vbuf + (k & 1) * kV;
+    double* rowk = colk + kMaxM;
+    const int kp = k >> 5, kr = k & 31;
+    if (ty == kr) {
+      double d = kp == 0 ? a[0][0] : kp == 1 ? a[1][1] : a[2][2];  // (k, k) at tx == kr
+      const double piv = __shfl(d, ((ty & 1) << 5) + kr, 64);
+      const bool okp = piv > 0.0;
+      const double ip = okp ? rcp_f64(piv) : 0.0;
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        const int j = tx + 32 * q;
+        const double v = kp == 0 ? a[0][q] : kp == 1 ? a[1][q] : a[2][q];
+        if (j < n) rowk[j] = v * ip;
+      }
+      if (tx == kr) {
+        rowk[kMaxM] = ip;
+        if (!okp) bad = 1;
+      }
+    }
+    if (tx == kr) {
+#pragma unroll
+      for (int p = 0; p < 3; p++) {
+        const int i = ty + 32 * p;
+        if (i < n) colk[i] = kp == 0 ? a[p][0] : kp == 1 ? a[p][1] : a[p][2];
+      }
     }
     __syncthreads();
-    for (int q = tid; q < m * nc; q += nt) {
-      const int r = q / nc, c = q % nc;
-      const double* drow = Dinv + (size_t)r * m;
-      double s = 0.0;
-      for (int k = 0; k < m; k++) s += drow[k] * panel[k * kPanel + c];
-      dst[(size_t)r * ldd + c0 + c] = s;
+    const double ip = rowk[kMaxM];
+    double ci[3], rj[3];
+#pragma unroll
+    for (int p = 0; p < 3; p++) ci[p] = colk[min(ty + 32 * p, n - 1)];
+#pragma unroll
+    for (int q = 0; q < 3; q++) rj[q] = rowk[min(tx + 32 * q, n - 1)];
+#pragma unroll
+    for (int p = 0; p < 3; p++)
+#pragma unroll
+      for (int q = 0; q < 3; q++) a[p][q] = fma(-ci[p], rj[q], a[p][q]);
+    // row k: a_kj / a_kk; column k: -a_ik / a_kk; (k, k): 1 / a_kk
+    if (ty == kr) {
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        if (kp == 0) a[0][q] = rj[q];
+        else if (kp == 1) a[1][q] = rj[q];
+        else a[2][q] = rj[q];
+      }
+    }
+    if (tx == kr) {
+#pragma unroll
+      for (int p = 0; p < 3; p++) {
+        const double v = (ty + 32 * p == k) ? ip : -ci[p] * ip;
+        if (kp == 0) a[p][0] = v;
+        else if (kp == 1) a[p][1] = v;
+        else a[p][2] = v;
+      }
     }
   }
   __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 3; p++)
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      const int i = ty + 32 * p, j = tx + 32 * q;
+      if (i < n && j < n) dst[(size_t)i * n + j] = a[p][q];
+    }
+  __syncthreads();
+  return bad == 0;
 }
 
-// C[M x N] (ldc) = (acc ? C : 0) + alpha * op(A) B, op(A) = A [M x K] (lda) or
-// A^T with A stored [K x M]; B [K x N] (ldb).  Global operands, LDS tiles,
-// fixed summation order.
-constexpr int kTM = 64, kTN = 64, kTK = 16;
-__device__ void wg_gemm(double* C, int ldc, const double* A, int lda, bool transA,
-                        const double* B, int ldb, int M, int N, int K, double alpha, bool acc,
-                        double* As, double* Bs) {
-  const int tid = threadIdx.x;  // 256 threads: 16 x 16, 4 x 4 outputs each
+// --- one-round-trip panel products (256 threads: tc = tid % 32 column,
+// tr = tid / 32 row group, rows tr + 8 a, a < 12)
+constexpr int kPT = 256;
+// Global -> LDS staging with the loads of 8 elements per thread issued back to
+// back before any is waited on (a plain load/store loop waits once per element:
+// one HBM round trip each).  src(q) gives the value of LDS element q.
+template <typename F>
+__device__ __forceinline__ void stage(double* dst, int total, F src) {
+  const int nt = blockDim.x;
+  for (int base = threadIdx.x; base < total; base += 8 * nt) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = base + u * nt;
+      v[u] = q < total ? src(q) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = base + u * nt;
+      if (q < total) dst[q] = v[u];
+    }
+  }
+}
+// As <- op(A) (M x K, row stride K): A row-major (lda) or, with trans, A^T
+// where A is stored K x M.  Loads only: the caller syncs.
+__device__ __forceinline__ void stage_a(const double* A, int lda, bool trans, int M, int K,
+                                        double* As) {
+  stage(As, M * K, [&](int q) {
+    const int r = q / K, k = q - r * K;
+    return trans ? A[(size_t)k * lda + r] : A[(size_t)r * lda + k];
+  });
+}
+// Bs <- columns [c0, c0 + nc) of B (K x *, row-major ldb) or of B^T (B stored
+// * x K) as K x kPW (zero-padded).  Loads only.
+__device__ __forceinline__ void stage_b(const double* B, int ldb, bool trans, int K, int c0, int nc,
+                                        double* Bs) {
+  stage(Bs, K * kPW, [&](int q) {
+    const int k = q / kPW, c = q - k * kPW;
+    double v = 0.0;
+    if (c < nc) v = trans ? B[(size_t)(c0 + c) * ldb + k] : B[(size_t)k * ldb + c0 + c];
+    return v;
+  });
+}
+// s[a] = sum_k As[r_a][k] Bs[k][tc], r_a = tr + 8 a, k ascending; K even.
+__device__ __forceinline__ void panel_dot(const double* As, int M, int K, const double* Bs,
+                                          double s[12]) {
+  const int tc = threadIdx.x & (kPW - 1), tr = threadIdx.x >> 5;
+  const int na = (M - tr + 7) >> 3;  // wave-uniform
+#pragma unroll
+  for (int a = 0; a < 12; a++) s[a] = 0.0;
+  for (int k = 0; k < K; k += 2) {
+    const double b0 = Bs[k * kPW + tc], b1 = Bs[(k + 1) * kPW + tc];
+#pragma unroll
+    for (int a = 0; a < 12; a++)
+      if (a < na) {
+        const double2 av = *reinterpret_cast<const double2*>(As + (tr + 8 * a) * K + k);
+        s[a] += av.x * b0;
+        s[a] += av.y * b1;
+      }
+  }
+}
+// C[rows, c0 + tc] = (acc ? C : 0) (+ alpha * s1 if use1) (+ alpha * s2 if use2)
+__device__ __forceinline__ void panel_store(double* C, int ldc, int M, int c0, int nc, double alpha,
+                                            bool acc, const double (&s1)[12], bool use1,
+                                            const double (&s2)[12], bool use2) {
+  const int tc = threadIdx.x & (kPW - 1), tr = threadIdx.x >> 5;
+  if (tc >= nc) return;
+#pragma unroll
+  for (int a = 0; a < 12; a++) {
+    const int r = tr + 8 * a;
+    if (r < M) {
+      double* cp = C + (size_t)r * ldc + c0 + tc;
+      double v = acc ? *cp : 0.0;
+      if (use1) v += alpha * s1[a];
+      if (use2) v += alpha * s2[a];
+      *cp = v;
+    }
+  }
+}
+
+// C[M x N] (ldc) = (acc ? C : 0) + alpha * A^T B with A stored [K x M] (lda),
+// B [K x N] (ldb), K <= kMaxM: 64 x 64 output tiles, each with ONE staging
+// round trip of its full-K operands; 256 threads, 4 x 4 outputs each.
+constexpr int kTM = 64, kTN = 64;
+__device__ void wg_gemm_tn(double* C, int ldc, const double* A, int lda, const double* B, int ldb,
+                           int M, int N, int K, double alpha, bool acc, double* As, double* Bs) {
+  const int tid = threadIdx.x;
   const int tr = tid / 16, tc = tid % 16;
   for (int i0 = 0; i0 < M; i0 += kTM)
     for (int j0 = 0; j0 < N; j0 += kTN) {
+      __syncthreads();
+      stage(As, K * kTM, [&](int q) {
+        const int k = q / kTM, i = q % kTM;
+        return (i0 + i < M) ? A[(size_t)k * lda + i0 + i] : 0.0;
+      });
+      stage(Bs, K * kTN, [&](int q) {
+        const int k = q / kTN, j = q % kTN;
+        return (j0 + j < N) ? B[(size_t)k * ldb + j0 + j] : 0.0;
+      });
+      __syncthreads();
       double s[4][4];
 #pragma unroll
       for (int a = 0; a < 4; a++)
 #pragma unroll
         for (int b = 0; b < 4; b++) s[a][b] = 0.0;
-      for (int k0 = 0; k0 < K; k0 += kTK) {
-        __syncthreads();
-        for (int q = tid; q < kTM * kTK; q += 256) {
-          const int i = q / kTK, k = q % kTK;
-          const int gi = i0 + i, gk = k0 + k;
-          double v = 0.0;
-          if (gi < M && gk < K) v = transA ? A[(size_t)gk * lda + gi] : A[(size_t)gi * lda + gk];
-          As[k * kTM + i] = v;
-        }
-        for (int q = tid; q < kTK * kTN; q += 256) {
-          const int k = q / kTN, j = q % kTN;
-          const int gk = k0 + k, gj = j0 + j;
-          Bs[q] = (gk < K && gj < N) ? B[(size_t)gk * ldb + gj] : 0.0;
-        }
-        __syncthreads();
+      for (int k = 0; k < K; k++) {
+        double av[4], bv[4];
 #pragma unroll
-        for (int k = 0; k < kTK; k++) {
-          double av[4], bv[4];
+        for (int a = 0; a < 4; a++) av[a] = As[k * kTM + tr + 16 * a];
 #pragma unroll
-          for (int a = 0; a < 4; a++) av[a] = As[k * kTM + tr + 16 * a];
+        for (int b = 0; b < 4; b++) bv[b] = Bs[k * kTN + tc + 16 * b];
 #pragma unroll
-          for (int b = 0; b < 4; b++) bv[b] = Bs[k * kTN + tc + 16 * b];
+        for (int a = 0; a < 4; a++)
 #pragma unroll
-          for (int a = 0; a < 4; a++)
-#pragma unroll
-            for (int b = 0; b < 4; b++) s[a][b] += av[a] * bv[b];
-        }
+          for (int b = 0; b < 4; b++) s[a][b] += av[a] * bv[b];
       }
 #pragma unroll
       for (int a = 0; a < 4; a++)
@@ -777,146 +939,246 @@ __device__ void wg_gemm(double* C, int ldc, const double* A, int lda, bool trans
   __syncthreads();
 }
 
+// LDS of the GJ kernels: inverse (kMaxM^2) | GJ vectors
+inline size_t gj_lds_bytes() { return sizeof(double) * ((size_t)kMaxM * kMaxM + 4 * kMaxM + 8); }
+// LDS of the panel kernels: A (kMaxM^2) | B panel (kMaxM x kPW)
+constexpr size_t kPanelLds = sizeof(double) * ((size_t)kMaxM * kMaxM + (size_t)kMaxM * kPW);
+
 // ------------------------------------------------- block cyclic reduction
 // Level lev: active superblocks are k * 2^lev, k < n.  Odd k are eliminated.
-__global__ void __launch_bounds__(kT) k_cr_a(int lev, Ws w, double* Lcur) {
+// top: the last remaining superblock (index 0) at the end.
+// Grids are sized by the host's bound and capped (kCrGrid); workgroups loop
+// over the level's real items, so a level costs no empty-workgroup rounds.
+constexpr int kCrGrid = 256;
+__device__ __forceinline__ int cr_nelim(const Meta* meta, int lev, bool top) {
+  if (top) return meta->nsb >= 1 ? 1 : 0;
+  const int n = level_count(meta->nsb, lev);
+  return n > 1 ? n / 2 : 0;
+}
+__device__ __forceinline__ int cr_nkept(const Meta* meta, int lev) {
+  const int n = level_count(meta->nsb, lev);
+  return n > 1 ? (n + 1) / 2 : 0;
+}
+
+__global__ void __launch_bounds__(kTB) k_cr_inv(int lev, int top, Ws w) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   Meta* meta = w.meta;
-  const int nsb = meta->nsb, m = meta->m, nr = 1 + 6 * meta->nB;
-  const int n = level_count(nsb, lev);
-  const int k = 2 * blockIdx.x + 1;
-  if (n <= 1 || k >= n) return;
-  const int st = 1 << lev, o = k * st, l = (k - 1) * st, r = (k + 1) * st;
-  const bool has_r = k + 1 < n;
-  double* Dinv = lds;
-  double* panel = Dinv + m * m;
-  double* vec = panel + m * kPanel;
-  const size_t mm = (size_t)m * m;
-  for (int q = threadIdx.x; q < m * m; q += blockDim.x) Dinv[q] = w.D[o * mm + q];
-  __syncthreads();
-  if (!wg_gj_inverse(Dinv, m, m, vec, vec + m)) {
-    if (threadIdx.x == 0) atomicOr(&meta->status, kStChol);
-  }
-  wg_lmul(Dinv, m, Lcur + l * mm, m, false, m, w.Y1 + o * mm, m, panel);  // D^-1 A[o, l]
-  if (has_r) wg_lmul(Dinv, m, Lcur + o * mm, m, true, m, w.Y2 + o * mm, m, panel);  // D^-1 A[o, r]
-  double* Ro = w.R + (size_t)o * m * nr;
-  wg_lmul(Dinv, m, Ro, nr, false, nr, Ro, nr, panel);  // Z_o = D^-1 R_o (in place)
-}
-
-__global__ void __launch_bounds__(kT) k_cr_b(int lev, Ws w, const double* Lcur, double* Lnext) {
-  __shared__ double As[kTM * kTK], Bs[kTK * kTN];
-  Meta* meta = w.meta;
-  const int nsb = meta->nsb, m = meta->m, nr = 1 + 6 * meta->nB;
-  const int n = level_count(nsb, lev);
-  const int k = 2 * blockIdx.x;
-  if (n <= 1 || k >= n) return;
-  const int st = 1 << lev, e = k * st;
-  const size_t mm = (size_t)m * m;
-  const bool has_l = k >= 1, has_r = k + 1 < n, has_r2 = k + 2 < n;
-  const int ol = (k - 1) * st, orr = (k + 1) * st;
-  double* De = w.D + e * mm;
-  double* Re = w.R + (size_t)e * m * nr;
-  if (has_l) {  // A[e, ol] = L[ol]
-    wg_gemm(De, m, Lcur + ol * mm, m, false, w.Y2 + ol * mm, m, m, m, m, -1.0, true, As, Bs);
-    wg_gemm(Re, nr, Lcur + ol * mm, m, false, w.R + (size_t)ol * m * nr, nr, m, nr, m, -1.0, true,
-            As, Bs);
-  }
-  if (has_r) {  // A[e, or] = L[e]^T
-    wg_gemm(De, m, Lcur + e * mm, m, true, w.Y1 + orr * mm, m, m, m, m, -1.0, true, As, Bs);
-    wg_gemm(Re, nr, Lcur + e * mm, m, true, w.R + (size_t)orr * m * nr, nr, m, nr, m, -1.0, true,
-            As, Bs);
-    if (has_r2)  // new coupling A'[r2, e] = -A[r2, or] D_or^-1 A[or, e] = -L[or] Y1[or]
-      wg_gemm(Lnext + e * mm, m, Lcur + orr * mm, m, false, w.Y1 + orr * mm, m, m, m, m, -1.0,
-              false, As, Bs);
+  const int cnt = cr_nelim(meta, lev, top), m = meta->m;
+  for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
+    const int k = top ? 0 : 2 * it + 1, o = k << lev;
+    double* D = w.D + (size_t)o * m * m;
+    if (!wg_gj_inverse_reg(D, m, m, D, lds)) {  // in place: D_o is not read again
+      if (threadIdx.x == 0) atomicOr(&meta->status, kStChol);
+    }
   }
 }
 
-// last remaining superblock (index 0): R_0 = D_0^-1 R_0
-__global__ void __launch_bounds__(kT) k_cr_top(Ws w) {
+// grid (panel, superblock): panels [0, kPanelsM) -> Y1, [kPanelsM, 2 kPanelsM)
+// -> Y2, then kPanelsR panels of R_o (in place).
+__global__ void __launch_bounds__(kPT) k_cr_mul(int lev, int top, Ws w, const double* Lcur) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  Meta* meta = w.meta;
-  const int nsb = meta->nsb, m = meta->m, nr = 1 + 6 * meta->nB;
-  if (nsb < 1) return;
-  double* Dinv = lds;
-  double* panel = Dinv + m * m;
-  double* vec = panel + m * kPanel;
-  for (int q = threadIdx.x; q < m * m; q += blockDim.x) Dinv[q] = w.D[q];
-  __syncthreads();
-  if (!wg_gj_inverse(Dinv, m, m, vec, vec + m)) {
-    if (threadIdx.x == 0) atomicOr(&meta->status, kStChol);
+  const Meta* meta = w.meta;
+  const int cnt = cr_nelim(meta, lev, top) * (2 * kPanelsM + kPanelsR);
+  const int m = meta->m, nr = 1 + 6 * meta->nB, st = 1 << lev;
+  const int n = level_count(meta->nsb, lev);
+  const size_t mm = (size_t)m * m;
+  double* As = lds;
+  double* Bs = As + kMaxM * kMaxM;
+  for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
+    const int e = it / (2 * kPanelsM + kPanelsR);
+    int pnl = it - e * (2 * kPanelsM + kPanelsR), seg;
+    const int k = top ? 0 : 2 * e + 1, o = k * st, l = (k - 1) * st;
+    const bool has_r = !top && k + 1 < n;
+    if (pnl < kPanelsM) seg = 0;
+    else if (pnl < 2 * kPanelsM) seg = 1, pnl -= kPanelsM;
+    else seg = 2, pnl -= 2 * kPanelsM;
+    const int c0 = pnl * kPW, ncol = seg == 2 ? nr : m;
+    if (c0 >= ncol || (top && seg < 2) || (seg == 1 && !has_r)) continue;  // block-uniform
+    const int nc = min(kPW, ncol - c0);
+    __syncthreads();
+    stage_a(w.D + o * mm, m, false, m, m, As);  // D_o^-1
+    double* Ro = w.R + (size_t)o * m * nr;
+    if (seg == 0) stage_b(Lcur + l * mm, m, false, m, c0, nc, Bs);       // A[o, l] = L[l]
+    else if (seg == 1) stage_b(Lcur + o * mm, m, true, m, c0, nc, Bs);   // A[o, r] = L[o]^T
+    else stage_b(Ro, nr, false, m, c0, nc, Bs);
+    __syncthreads();
+    double s[12];
+    panel_dot(As, m, m, Bs, s);
+    if (seg == 0) panel_store(w.Y1 + o * mm, m, m, c0, nc, 1.0, false, s, true, s, false);
+    else if (seg == 1) panel_store(w.Y2 + o * mm, m, m, c0, nc, 1.0, false, s, true, s, false);
+    else panel_store(Ro, nr, m, c0, nc, 1.0, false, s, true, s, false);
   }
-  wg_lmul(Dinv, m, w.R, nr, false, nr, w.R, nr, panel);
 }
 
-// back substitution of level lev: x_o = Z_o - Y1 x_l - Y2 x_r
-__global__ void __launch_bounds__(kT) k_cr_back(int lev, Ws w) {
-  __shared__ double As[kTM * kTK], Bs[kTK * kTN];
-  Meta* meta = w.meta;
-  const int nsb = meta->nsb, m = meta->m, nr = 1 + 6 * meta->nB;
-  const int n = level_count(nsb, lev);
-  const int k = 2 * blockIdx.x + 1;
-  if (n <= 1 || k >= n) return;
-  const int st = 1 << lev, o = k * st, l = (k - 1) * st, r = (k + 1) * st;
+// grid (panel, kept superblock): [D_e | R_e | L'_e] column panels.
+//   D_e -= L[ol] Y2[ol] + L[e]^T Y1[or];  R_e -= L[ol] R[ol] + L[e]^T R[or]
+//   L'_e = -L[or] Y1[or]  (new coupling A'[r2, e])
+__global__ void __launch_bounds__(kPT) k_cr_b(int lev, Ws w, const double* Lcur, double* Lnext) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const Meta* meta = w.meta;
+  constexpr int kP = 2 * kPanelsM + kPanelsR;
+  const int n = level_count(meta->nsb, lev), cnt = cr_nkept(meta, lev) * kP;
+  const int m = meta->m, nr = 1 + 6 * meta->nB, st = 1 << lev;
   const size_t mm = (size_t)m * m, mr = (size_t)m * nr;
-  double* Ro = w.R + o * mr;
-  wg_gemm(Ro, nr, w.Y1 + o * mm, m, false, w.R + l * mr, nr, m, nr, m, -1.0, true, As, Bs);
-  if (k + 1 < n)
-    wg_gemm(Ro, nr, w.Y2 + o * mm, m, false, w.R + r * mr, nr, m, nr, m, -1.0, true, As, Bs);
+  double* As = lds;
+  double* Bs = As + kMaxM * kMaxM;
+  for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
+    const int kq = it / kP;
+    int pnl = it - kq * kP, seg;
+    const int k = 2 * kq, e = k * st;
+    const bool has_l = k >= 1, has_r = k + 1 < n, has_r2 = k + 2 < n;
+    const int ol = (k - 1) * st, orr = (k + 1) * st;
+    if (pnl < kPanelsM) seg = 0;
+    else if (pnl < kPanelsM + kPanelsR) seg = 1, pnl -= kPanelsM;
+    else seg = 2, pnl -= kPanelsM + kPanelsR;
+    const int c0 = pnl * kPW, ncol = seg == 1 ? nr : m;
+    if (c0 >= ncol || (seg == 2 && !has_r2) || (!has_l && !has_r)) continue;  // block-uniform
+    const int nc = min(kPW, ncol - c0);
+    double s1[12], s2[12];
+    __syncthreads();
+    if (seg == 2) {
+      stage_a(Lcur + orr * mm, m, false, m, m, As);
+      stage_b(w.Y1 + orr * mm, m, false, m, c0, nc, Bs);
+      __syncthreads();
+      panel_dot(As, m, m, Bs, s1);
+      panel_store(Lnext + e * mm, m, m, c0, nc, -1.0, false, s1, true, s1, false);
+      continue;
+    }
+    double* C = seg == 0 ? w.D + e * mm : w.R + e * mr;
+    const int ldc = seg == 0 ? m : nr;
+    if (has_l) {  // A[e, ol] = L[ol]
+      stage_a(Lcur + ol * mm, m, false, m, m, As);
+      if (seg == 0) stage_b(w.Y2 + ol * mm, m, false, m, c0, nc, Bs);
+      else stage_b(w.R + ol * mr, nr, false, m, c0, nc, Bs);
+      __syncthreads();
+      panel_dot(As, m, m, Bs, s1);
+    }
+    if (has_r) {  // A[e, or] = L[e]^T
+      __syncthreads();
+      stage_a(Lcur + e * mm, m, true, m, m, As);
+      if (seg == 0) stage_b(w.Y1 + orr * mm, m, false, m, c0, nc, Bs);
+      else stage_b(w.R + orr * mr, nr, false, m, c0, nc, Bs);
+      __syncthreads();
+      panel_dot(As, m, m, Bs, s2);
+    }
+    panel_store(C, ldc, m, c0, nc, -1.0, true, s1, has_l, s2, has_r);
+  }
 }
 
-// border Schur complement: [Sb | rb] = [Cb | yB] - BT^T [X | z0]
-__global__ void k_border_schur(Ws w) {
+// grid (panel of R, eliminated superblock): x_o = Z_o - Y1 x_l - Y2 x_r
+__global__ void __launch_bounds__(kPT) k_cr_back(int lev, Ws w) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const Meta* meta = w.meta;
+  const int n = level_count(meta->nsb, lev), cnt = cr_nelim(meta, lev, false) * kPanelsR;
+  const int m = meta->m, nr = 1 + 6 * meta->nB, st = 1 << lev;
+  const size_t mm = (size_t)m * m, mr = (size_t)m * nr;
+  double* As = lds;
+  double* Bs = As + kMaxM * kMaxM;
+  for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
+    const int e = it / kPanelsR, c0 = (it - e * kPanelsR) * kPW;
+    if (c0 >= nr) continue;  // block-uniform
+    const int nc = min(kPW, nr - c0);
+    const int k = 2 * e + 1, o = k * st, l = (k - 1) * st, r = (k + 1) * st;
+    double s1[12], s2[12];
+    __syncthreads();
+    stage_a(w.Y1 + o * mm, m, false, m, m, As);
+    stage_b(w.R + l * mr, nr, false, m, c0, nc, Bs);
+    __syncthreads();
+    panel_dot(As, m, m, Bs, s1);
+    const bool has_r = k + 1 < n;
+    if (has_r) {
+      __syncthreads();
+      stage_a(w.Y2 + o * mm, m, false, m, m, As);
+      stage_b(w.R + r * mr, nr, false, m, c0, nc, Bs);
+      __syncthreads();
+      panel_dot(As, m, m, Bs, s2);
+    }
+    panel_store(w.R + o * mr, nr, m, c0, nc, -1.0, true, s1, true, s2, has_r);
+  }
+}
+
+// border Schur complement [Sb | rb] = [Cb | yB] - BT^T [X | z0], in two
+// passes: workgroup g sums BT_sb^T [X_sb | z0_sb] over sb = g, g + kBP, ...
+// into its own partial (no atomics), then a fixed-order sum over the groups.
+__global__ void __launch_bounds__(256) k_border_part(Ws w) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const Meta* meta = w.meta;
+  const int nB = meta->nB, nsb = meta->nsb, m = meta->m;
+  if (nB == 0 || nB > kMaxBorder) return;
+  const int nb6 = 6 * nB, nr = 1 + nb6, g = blockIdx.x;
+  double* part = w.Pb + (size_t)g * nb6 * nr;
+  for (int sb = g; sb < nsb; sb += kBP) {
+    const double* bt = w.BT + (size_t)sb * m * nr + 1;  // [m][nr], border columns 1..nb6
+    const double* x = w.R + (size_t)sb * m * nr;
+    wg_gemm_tn(part, nr, bt, nr, x, nr, nb6, nr, m, 1.0, sb != g, lds, lds + kMaxM * kTM);
+  }
+}
+
+__global__ void k_border_reduce(Ws w) {
   const Meta* meta = w.meta;
   const int nB = meta->nB;
   if (nB == 0 || nB > kMaxBorder) return;
-  const int nb6 = 6 * nB, nr = 1 + nb6, nsb = meta->nsb, m = meta->m;
+  const int nb6 = 6 * nB, nr = 1 + nb6, ng = min(meta->nsb, kBP);
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nb6 * nr) return;
   const int r = q / nr, c = q % nr;  // c == 0: rhs, c >= 1: Sb column c - 1
   double s = 0.0;
-  for (int sb = 0; sb < nsb; sb++) {
-    const double* bt = w.BT + (size_t)sb * m * nr;
-    const double* x = w.R + (size_t)sb * m * nr;
-    for (int row = 0; row < m; row++) s += bt[(size_t)row * nr + 1 + r] * x[(size_t)row * nr + c];
-  }
+#pragma unroll 8
+  for (int g = 0; g < ng; g++) s += w.Pb[(size_t)g * nb6 * nr + q];
   if (c == 0) w.rb[r] -= s;
   else w.Cb[(size_t)r * nb6 + c - 1] -= s;
 }
 
-__global__ void __launch_bounds__(kT) k_border_solve(Ws w) {
-  __shared__ double vec[2 * kMaxNB6];
+// dense border solve: register Gauss-Jordan for 6 nB <= kMaxM, else in place in HBM
+__global__ void __launch_bounds__(kTB) k_border_solve(Ws w) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
   Meta* meta = w.meta;
   const int nB = meta->nB;
   if (nB == 0 || nB > kMaxBorder) return;
   const int nb6 = 6 * nB;
-  if (!wg_gj_inverse(w.Cb, nb6, nb6, vec, vec + nb6)) {
-    if (threadIdx.x == 0) atomicOr(&meta->status, kStChol);
+  double* rb = lds + kMaxM * kMaxM + 4 * kMaxM + 8;
+  const double* inv;
+  bool ok;
+  if (nb6 <= kMaxM) {
+    for (int q = threadIdx.x; q < nb6; q += blockDim.x) rb[q] = w.rb[q];
+    ok = wg_gj_inverse_reg(w.Cb, nb6, nb6, lds, lds + kMaxM * kMaxM);
+    inv = lds;
+  } else {
+    ok = wg_gj_inverse(w.Cb, nb6, nb6, lds, lds + nb6);
+    for (int q = threadIdx.x; q < nb6; q += blockDim.x) rb[q] = w.rb[q];
+    __syncthreads();
+    inv = w.Cb;
   }
+  if (!ok && threadIdx.x == 0) atomicOr(&meta->status, kStChol);
   for (int r = threadIdx.x; r < nb6; r += blockDim.x) {
     double s = 0.0;
-    for (int k = 0; k < nb6; k++) s += w.Cb[(size_t)r * nb6 + k] * w.rb[k];
+    for (int k = 0; k < nb6; k++) s += inv[(size_t)r * nb6 + k] * rb[k];
     w.dXB[r] = s;
   }
 }
 
 // dX in pose order: interior x = z0 - X dXB; border dXB.  Failed solve -> 0.
-__global__ void k_final_dx(int N, Ws w) {
+__global__ void __launch_bounds__(256) k_final_dx(int N, Ws w) {
+  __shared__ double xb[kMaxNB6];
+  const Meta* meta = w.meta;
+  const int nB = min(meta->nB, kMaxBorder);
+  for (int c = threadIdx.x; c < 6 * nB; c += blockDim.x) xb[c] = w.dXB[c];
+  __syncthreads();
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= 6 * N) return;
-  const Meta* meta = w.meta;
   if (meta->status & (kStChol | kStBorder)) {
     w.dX[q] = 0.0;
     return;
   }
-  const int a = q / 6, rr = q % 6, g = meta->g, m = meta->m, nB = meta->nB, nr = 1 + 6 * nB;
+  const int a = q / 6, rr = q % 6, g = meta->g, m = meta->m, nr = 1 + 6 * nB;
   double v;
   const int ca = w.cidx[a];
   if (ca >= 0) {
     const double* x = w.R + (size_t)(ca / g) * m * nr + (size_t)((ca % g) * 6 + rr) * nr;
     v = x[0];
-    for (int c = 0; c < 6 * nB; c++) v -= x[1 + c] * w.dXB[c];
+    for (int c = 0; c < 6 * nB; c++) v -= x[1 + c] * xb[c];
   } else {
-    v = w.dXB[6 * w.bidx[a] + rr];
+    v = xb[6 * w.bidx[a] + rr];
   }
   w.dX[q] = v;
 }
@@ -983,10 +1245,6 @@ __global__ void k_clear_chol(Ws w) {
 
 inline int grid_of(long long n, int t = kT) { return (int)std::max<long long>(1, (n + t - 1) / t); }
 
-inline size_t cr_lds_bytes() {
-  return sizeof(double) * ((size_t)kMaxM * kMaxM + (size_t)kMaxM * kPanel + 2 * kMaxM);
-}
-
 inline int cr_levels(int N) {
   int n = N, L = 0;
   while (n > 1) {
@@ -999,10 +1257,12 @@ inline int cr_levels(int N) {
 static void ensure_attrs() {
   static bool done = false;
   if (done) return;
-  (void)hipFuncSetAttribute((const void*)k_cr_a, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      (int)cr_lds_bytes());
-  (void)hipFuncSetAttribute((const void*)k_cr_top, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      (int)cr_lds_bytes());
+  for (const void* f : {(const void*)k_cr_inv, (const void*)k_border_solve})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(gj_lds_bytes() + sizeof(double) * kMaxNB6));
+  for (const void* f : {(const void*)k_cr_mul, (const void*)k_cr_b, (const void*)k_cr_back,
+                        (const void*)k_border_part})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPanelLds);
   done = true;
 }
 
@@ -1101,14 +1361,20 @@ int gba_solve_update(float* poses, float* patches, int E, int P, int t0, int t1,
     const int L = cr_levels(N);
     double* Lo[2] = {w.Lo0, w.Lo1};
     int n = N;  // upper bound of the superblock count at each level
+    const size_t lg = gj_lds_bytes() + sizeof(double) * kMaxNB6;
+    constexpr int kP = 2 * kPanelsM + kPanelsR;
+    auto cap = [](long long v) { return (int)std::max(1LL, std::min<long long>(v, kCrGrid)); };
     for (int lev = 0; lev < L; lev++) {
-      hipLaunchKernelGGL(k_cr_a, dim3(std::max(1, n / 2)), dim3(kT), cr_lds_bytes(), s, lev, w,
-                         Lo[lev & 1]);
-      hipLaunchKernelGGL(k_cr_b, dim3(std::max(1, (n + 1) / 2)), dim3(kT), 0, s, lev, w,
+      const int ne = n / 2, nk = (n + 1) / 2;
+      hipLaunchKernelGGL(k_cr_inv, dim3(cap(ne)), dim3(kTB), lg, s, lev, 0, w);
+      hipLaunchKernelGGL(k_cr_mul, dim3(cap((long long)ne * kP)), dim3(kPT), kPanelLds, s, lev, 0,
+                         w, Lo[lev & 1]);
+      hipLaunchKernelGGL(k_cr_b, dim3(cap((long long)nk * kP)), dim3(kPT), kPanelLds, s, lev, w,
                          Lo[lev & 1], Lo[(lev + 1) & 1]);
       n = (n + 1) >> 1;
     }
-    hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(kT), cr_lds_bytes(), s, w);
+    hipLaunchKernelGGL(k_cr_inv, dim3(1), dim3(kTB), lg, s, L, 1, w);
+    hipLaunchKernelGGL(k_cr_mul, dim3(kP), dim3(kPT), kPanelLds, s, L, 1, w, Lo[L & 1]);
     n = N;
     int nl[32];
     for (int lev = 0; lev < L; lev++) {
@@ -1116,10 +1382,12 @@ int gba_solve_update(float* poses, float* patches, int E, int P, int t0, int t1,
       n = (n + 1) >> 1;
     }
     for (int lev = L - 1; lev >= 0; lev--)
-      hipLaunchKernelGGL(k_cr_back, dim3(std::max(1, nl[lev] / 2)), dim3(kT), 0, s, lev, w);
-    hipLaunchKernelGGL(k_border_schur, dim3(grid_of((long long)kMaxNB6 * (kMaxNB6 + 1))),
+      hipLaunchKernelGGL(k_cr_back, dim3(cap((long long)(nl[lev] / 2) * kPanelsR)), dim3(kPT),
+                         kPanelLds, s, lev, w);
+    hipLaunchKernelGGL(k_border_part, dim3(kBP), dim3(256), kPanelLds, s, w);
+    hipLaunchKernelGGL(k_border_reduce, dim3(grid_of((long long)kMaxNB6 * (kMaxNB6 + 1))),
                        dim3(kT), 0, s, w);
-    hipLaunchKernelGGL(k_border_solve, dim3(1), dim3(kT), 0, s, w);
+    hipLaunchKernelGGL(k_border_solve, dim3(1), dim3(kTB), lg, s, w);
     hipLaunchKernelGGL(k_final_dx, dim3(grid_of(6 * N)), dim3(kT), 0, s, N, w);
   }
   hipLaunchKernelGGL(k_update, dim3(grid_of((long long)N + E)), dim3(kT), 0, s, poses, patches, E,
