@@ -719,15 +719,19 @@ __device__ __forceinline__ double rcp_f64(double p) {
   return fma(r, e, r);
 }
 
-// Gauss-Jordan inverse (no pivoting; SPD) of the n x n matrix src (row stride
-// lda) into dst (row stride n; global or LDS; may alias src: every load
-// happens before the first barrier).  1024 threads; thread (ty, tx) owns
-// entries (ty + 32 p, tx + 32 q).  Per pivot k ONE barrier: the owners of row
-// k (one half-wave) take the pivot by a lane shuffle, publish the scaled row
-// a_kj / a_kk and 1 / a_kk, the owners of column k publish it (parity
-// double-buffered LDS: a writer of step k + 2 has passed the barrier of step
-// k + 1, so every reader of step k is done); every entry is then one FMA.
-__device__ bool wg_gj_inverse_reg(const double* src, int n, int lda, double* dst, double* vbuf) {
+// Block Gauss-Jordan inverse (no pivoting; SPD), 6 x 6 pivot blocks, of the
+// n x n matrix src (n = 6 nb <= kMaxM, row stride lda) into dst (row stride n;
+// global or LDS; may alias src: every load happens before the first barrier).
+// 1024 threads; thread (ty, tx) keeps entries (ty + 32 p, tx + 32 q) in
+// registers.  TWO barriers per block step (a scalar Gauss-Jordan needs one per
+// pivot, six per block, each on the pivot's dependency chain): (1) the owners publish the raw block rows Rw (6 x n) and
+// block columns Cw (n x 6) (parity double-buffered); (2) wave 0 inverts the
+// pivot P = A[b, b] (one entry per lane, pivot row / column by shuffles) and
+// forms W = P^-1 Rw and V = Cw P^-1; then every entry outside the block gets
+// a -= Cw_i . W_j (6 FMAs), block rows W, block columns -V, the pivot P^-1.
+// vbuf: 2 (Rw + Cw) + W + V + P^-1 = 2 * 12 kMaxM + 12 kMaxM + 36 doubles.
+constexpr size_t kBgjDoubles = 36 * (size_t)kMaxM + 40;
+__device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda, double* dst, double* vbuf) {
   __shared__ int bad;
   const int tid = threadIdx.x, ty = tid >> 5, tx = tid & 31;
   double a[3][3];
@@ -739,61 +743,104 @@ __device__ bool wg_gj_inverse_reg(const double* src, int n, int lda, double* dst
       a[p][q] = (i < n && j < n) ? src[(size_t)i * lda + j] : 0.0;
     }
   if (tid == 0) bad = 0;
-  constexpr int kV = 2 * kMaxM + 2;
-  for (int k = 0; k < n; k++) {
-    double* colk = vbuf + (k & 1) * kV;
-    double* rowk = colk + kMaxM;
-    const int kp = k >> 5, kr = k & 31;
-    if (ty == kr) {
-      double d = kp == 0 ? a[0][0] : kp == 1 ? a[1][1] : a[2][2];  // (k, k) at tx == kr
-      const double piv = __shfl(d, ((ty & 1) << 5) + kr, 64);
-      const bool okp = piv > 0.0;
-      const double ip = okp ? rcp_f64(piv) : 0.0;
+  double* W = vbuf + 24 * kMaxM;  // [6][kMaxM]
+  double* V = W + 6 * kMaxM;      // [kMaxM][6]
+  double* Pi = V + 6 * kMaxM;     // [36]
+  const int nb = n / 6;
+  for (int K = 0; K < nb; K++) {
+    const int b0 = 6 * K;
+    double* Rw = vbuf + (K & 1) * 12 * kMaxM;  // [6][kMaxM]
+    double* Cw = Rw + 6 * kMaxM;                // [kMaxM][6]
+    // (1) publish: a thread owns at most one row and one column of the block
+    const int dr = (ty - b0) & 31, dc = (tx - b0) & 31;
+    if (dr < 6) {
+      const int r = b0 + dr, rp = r >> 5;
 #pragma unroll
       for (int q = 0; q < 3; q++) {
         const int j = tx + 32 * q;
-        const double v = kp == 0 ? a[0][q] : kp == 1 ? a[1][q] : a[2][q];
-        if (j < n) rowk[j] = v * ip;
-      }
-      if (tx == kr) {
-        rowk[kMaxM] = ip;
-        if (!okp) bad = 1;
+        const double v = rp == 0 ? a[0][q] : rp == 1 ? a[1][q] : a[2][q];
+        if (j < n) Rw[dr * kMaxM + j] = v;
       }
     }
-    if (tx == kr) {
+    if (dc < 6) {
+      const int c = b0 + dc, cq = c >> 5;
 #pragma unroll
       for (int p = 0; p < 3; p++) {
         const int i = ty + 32 * p;
-        if (i < n) colk[i] = kp == 0 ? a[p][0] : kp == 1 ? a[p][1] : a[p][2];
+        const double v = cq == 0 ? a[p][0] : cq == 1 ? a[p][1] : a[p][2];
+        if (i < n) Cw[i * 6 + dc] = v;
       }
     }
     __syncthreads();
-    const double ip = rowk[kMaxM];
-    double ci[3], rj[3];
+    // (2) wave 0: P^-1, W, V
+    if (tid < kWave) {
+      // lane 6 r + c holds P[r][c]; pivot row / column by lane shuffles
+      const int lr = min(tid, 35) / 6, lc = min(tid, 35) % 6;
+      double x = Rw[lr * kMaxM + b0 + lc];
+      bool ok = true;
 #pragma unroll
-    for (int p = 0; p < 3; p++) ci[p] = colk[min(ty + 32 * p, n - 1)];
+      for (int t = 0; t < 6; t++) {
+        const double piv = __shfl(x, 7 * t, 64);
+        const double rowv = __shfl(x, 6 * t + lc, 64);
+        const double colv = __shfl(x, 6 * lr + t, 64);
+        ok = ok && piv > 0.0;
+        const double ip = piv > 0.0 ? rcp_f64(piv) : 0.0;
+        if (lr != t && lc != t) x = fma(-colv, rowv * ip, x);
+        else if (lr == t && lc != t) x = rowv * ip;
+        else if (lr != t) x = -colv * ip;
+        else x = ip;
+      }
+      if (!ok && tid == 0) bad = 1;
+      if (tid < 36) Pi[tid] = x;
+      wave_lds_sync();
+      for (int q = tid; q < 6 * n; q += kWave) {
+        const int d = q / n, j = q - d * n;  // W[d][j]
+        const int i = q / 6, e = q - i * 6;  // V[i][e]
+        double sw = 0.0, sv = 0.0;
 #pragma unroll
-    for (int q = 0; q < 3; q++) rj[q] = rowk[min(tx + 32 * q, n - 1)];
-#pragma unroll
-    for (int p = 0; p < 3; p++)
-#pragma unroll
-      for (int q = 0; q < 3; q++) a[p][q] = fma(-ci[p], rj[q], a[p][q]);
-    // row k: a_kj / a_kk; column k: -a_ik / a_kk; (k, k): 1 / a_kk
-    if (ty == kr) {
-#pragma unroll
-      for (int q = 0; q < 3; q++) {
-        if (kp == 0) a[0][q] = rj[q];
-        else if (kp == 1) a[1][q] = rj[q];
-        else a[2][q] = rj[q];
+        for (int u = 0; u < 6; u++) {
+          sw = fma(Pi[d * 6 + u], Rw[u * kMaxM + j], sw);
+          sv = fma(Cw[i * 6 + u], Pi[u * 6 + e], sv);
+        }
+        W[d * kMaxM + j] = sw;
+        V[i * 6 + e] = sv;
       }
     }
-    if (tx == kr) {
+    __syncthreads();
+    // (3) update
+    double wj[3][6];
 #pragma unroll
-      for (int p = 0; p < 3; p++) {
-        const double v = (ty + 32 * p == k) ? ip : -ci[p] * ip;
-        if (kp == 0) a[p][0] = v;
-        else if (kp == 1) a[p][1] = v;
-        else a[p][2] = v;
+    for (int q = 0; q < 3; q++) {
+      const int j = min(tx + 32 * q, n - 1);
+#pragma unroll
+      for (int u = 0; u < 6; u++) wj[q][u] = W[u * kMaxM + j];
+    }
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+      const int i = ty + 32 * p;
+      if (i >= n) continue;  // wave-uniform for p = 2
+      double ci[6];
+#pragma unroll
+      for (int u = 0; u < 6; u++) ci[u] = Cw[i * 6 + u];
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        double v = a[p][q];
+#pragma unroll
+        for (int u = 0; u < 6; u++) v = fma(-ci[u], wj[q][u], v);
+        a[p][q] = v;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 3; p++) {
+      const int ri = ty + 32 * p - b0;
+      const bool inr = ri >= 0 && ri < 6;
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        const int cj = tx + 32 * q - b0;
+        const bool inc = cj >= 0 && cj < 6;
+        if (inr && inc) a[p][q] = Pi[ri * 6 + cj];
+        else if (inr) a[p][q] = W[ri * kMaxM + min(tx + 32 * q, n - 1)];
+        else if (inc) a[p][q] = -V[min(ty + 32 * p, n - 1) * 6 + cj];
       }
     }
   }
@@ -940,9 +987,16 @@ __device__ void wg_gemm_tn(double* C, int ldc, const double* A, int lda, const d
 }
 
 // LDS of the GJ kernels: inverse (kMaxM^2) | GJ vectors
-inline size_t gj_lds_bytes() { return sizeof(double) * ((size_t)kMaxM * kMaxM + 4 * kMaxM + 8); }
+inline size_t gj_lds_bytes() { return sizeof(double) * ((size_t)kMaxM * kMaxM + kBgjDoubles); }
 // LDS of the panel kernels: A (kMaxM^2) | B panel (kMaxM x kPW)
 constexpr size_t kPanelLds = sizeof(double) * ((size_t)kMaxM * kMaxM + (size_t)kMaxM * kPW);
+// k_cr_b / k_cr_back stage both products' operands at once when they fit
+constexpr size_t kPanelLds2 = 160 * 1024;
+// (layout: A at 0, B at kMaxM^2, second A / B right after the first B)
+__device__ __forceinline__ bool two_fit(int m) {
+  return sizeof(double) * ((size_t)kMaxM * kMaxM + (size_t)m * m + 2 * (size_t)m * kPW) <=
+         kPanelLds2;
+}
 
 // ------------------------------------------------- block cyclic reduction
 // Level lev: active superblocks are k * 2^lev, k < n.  Odd k are eliminated.
@@ -967,7 +1021,7 @@ __global__ void __launch_bounds__(kTB) k_cr_inv(int lev, int top, Ws w) {
   for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
     const int k = top ? 0 : 2 * it + 1, o = k << lev;
     double* D = w.D + (size_t)o * m * m;
-    if (!wg_gj_inverse_reg(D, m, m, D, lds)) {  // in place: D_o is not read again
+    if (!wg_bgj_inverse(D, m, m, D, lds)) {  // in place: D_o is not read again
       if (threadIdx.x == 0) atomicOr(&meta->status, kStChol);
     }
   }
@@ -1046,20 +1100,34 @@ __global__ void __launch_bounds__(kPT) k_cr_b(int lev, Ws w, const double* Lcur,
     }
     double* C = seg == 0 ? w.D + e * mm : w.R + e * mr;
     const int ldc = seg == 0 ? m : nr;
-    if (has_l) {  // A[e, ol] = L[ol]
+    // A[e, ol] = L[ol] (B: Y2[ol] | R[ol]); A[e, or] = L[e]^T (B: Y1[or] | R[or])
+    const double* B1 = seg == 0 ? w.Y2 + ol * mm : w.R + ol * mr;
+    const double* B2 = seg == 0 ? w.Y1 + orr * mm : w.R + orr * mr;
+    const int ldb = seg == 0 ? m : nr;
+    if (has_l && has_r && two_fit(m)) {  // one round trip for both products
+      double* As2 = Bs + m * kPW;
+      double* Bs2 = As2 + m * m;
       stage_a(Lcur + ol * mm, m, false, m, m, As);
-      if (seg == 0) stage_b(w.Y2 + ol * mm, m, false, m, c0, nc, Bs);
-      else stage_b(w.R + ol * mr, nr, false, m, c0, nc, Bs);
+      stage_b(B1, ldb, false, m, c0, nc, Bs);
+      stage_a(Lcur + e * mm, m, true, m, m, As2);
+      stage_b(B2, ldb, false, m, c0, nc, Bs2);
       __syncthreads();
       panel_dot(As, m, m, Bs, s1);
-    }
-    if (has_r) {  // A[e, or] = L[e]^T
-      __syncthreads();
-      stage_a(Lcur + e * mm, m, true, m, m, As);
-      if (seg == 0) stage_b(w.Y1 + orr * mm, m, false, m, c0, nc, Bs);
-      else stage_b(w.R + orr * mr, nr, false, m, c0, nc, Bs);
-      __syncthreads();
-      panel_dot(As, m, m, Bs, s2);
+      panel_dot(As2, m, m, Bs2, s2);
+    } else {
+      if (has_l) {
+        stage_a(Lcur + ol * mm, m, false, m, m, As);
+        stage_b(B1, ldb, false, m, c0, nc, Bs);
+        __syncthreads();
+        panel_dot(As, m, m, Bs, s1);
+      }
+      if (has_r) {
+        __syncthreads();
+        stage_a(Lcur + e * mm, m, true, m, m, As);
+        stage_b(B2, ldb, false, m, c0, nc, Bs);
+        __syncthreads();
+        panel_dot(As, m, m, Bs, s2);
+      }
     }
     panel_store(C, ldc, m, c0, nc, -1.0, true, s1, has_l, s2, has_r);
   }
@@ -1081,17 +1149,29 @@ __global__ void __launch_bounds__(kPT) k_cr_back(int lev, Ws w) {
     const int k = 2 * e + 1, o = k * st, l = (k - 1) * st, r = (k + 1) * st;
     double s1[12], s2[12];
     __syncthreads();
-    stage_a(w.Y1 + o * mm, m, false, m, m, As);
-    stage_b(w.R + l * mr, nr, false, m, c0, nc, Bs);
-    __syncthreads();
-    panel_dot(As, m, m, Bs, s1);
     const bool has_r = k + 1 < n;
-    if (has_r) {
+    if (has_r && two_fit(m)) {  // one round trip for both products
+      double* As2 = Bs + m * kPW;
+      double* Bs2 = As2 + m * m;
+      stage_a(w.Y1 + o * mm, m, false, m, m, As);
+      stage_b(w.R + l * mr, nr, false, m, c0, nc, Bs);
+      stage_a(w.Y2 + o * mm, m, false, m, m, As2);
+      stage_b(w.R + r * mr, nr, false, m, c0, nc, Bs2);
       __syncthreads();
-      stage_a(w.Y2 + o * mm, m, false, m, m, As);
-      stage_b(w.R + r * mr, nr, false, m, c0, nc, Bs);
+      panel_dot(As, m, m, Bs, s1);
+      panel_dot(As2, m, m, Bs2, s2);
+    } else {
+      stage_a(w.Y1 + o * mm, m, false, m, m, As);
+      stage_b(w.R + l * mr, nr, false, m, c0, nc, Bs);
       __syncthreads();
-      panel_dot(As, m, m, Bs, s2);
+      panel_dot(As, m, m, Bs, s1);
+      if (has_r) {
+        __syncthreads();
+        stage_a(w.Y2 + o * mm, m, false, m, m, As);
+        stage_b(w.R + r * mr, nr, false, m, c0, nc, Bs);
+        __syncthreads();
+        panel_dot(As, m, m, Bs, s2);
+      }
     }
     panel_store(w.R + o * mr, nr, m, c0, nc, -1.0, true, s1, true, s2, has_r);
   }
@@ -1136,12 +1216,12 @@ __global__ void __launch_bounds__(kTB) k_border_solve(Ws w) {
   const int nB = meta->nB;
   if (nB == 0 || nB > kMaxBorder) return;
   const int nb6 = 6 * nB;
-  double* rb = lds + kMaxM * kMaxM + 4 * kMaxM + 8;
+  double* rb = lds + kMaxM * kMaxM + kBgjDoubles;
   const double* inv;
   bool ok;
   if (nb6 <= kMaxM) {
     for (int q = threadIdx.x; q < nb6; q += blockDim.x) rb[q] = w.rb[q];
-    ok = wg_gj_inverse_reg(w.Cb, nb6, nb6, lds, lds + kMaxM * kMaxM);
+    ok = wg_bgj_inverse(w.Cb, nb6, nb6, lds, lds + kMaxM * kMaxM);
     inv = lds;
   } else {
     ok = wg_gj_inverse(w.Cb, nb6, nb6, lds, lds + nb6);
@@ -1260,9 +1340,10 @@ static void ensure_attrs() {
   for (const void* f : {(const void*)k_cr_inv, (const void*)k_border_solve})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)(gj_lds_bytes() + sizeof(double) * kMaxNB6));
-  for (const void* f : {(const void*)k_cr_mul, (const void*)k_cr_b, (const void*)k_cr_back,
-                        (const void*)k_border_part})
+  for (const void* f : {(const void*)k_cr_mul, (const void*)k_border_part})
     (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPanelLds);
+  for (const void* f : {(const void*)k_cr_b, (const void*)k_cr_back})
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPanelLds2);
   done = true;
 }
 
@@ -1369,7 +1450,7 @@ int gba_solve_update(float* poses, float* patches, int E, int P, int t0, int t1,
       hipLaunchKernelGGL(k_cr_inv, dim3(cap(ne)), dim3(kTB), lg, s, lev, 0, w);
       hipLaunchKernelGGL(k_cr_mul, dim3(cap((long long)ne * kP)), dim3(kPT), kPanelLds, s, lev, 0,
                          w, Lo[lev & 1]);
-      hipLaunchKernelGGL(k_cr_b, dim3(cap((long long)nk * kP)), dim3(kPT), kPanelLds, s, lev, w,
+      hipLaunchKernelGGL(k_cr_b, dim3(cap((long long)nk * kP)), dim3(kPT), kPanelLds2, s, lev, w,
                          Lo[lev & 1], Lo[(lev + 1) & 1]);
       n = (n + 1) >> 1;
     }
@@ -1383,7 +1464,7 @@ int gba_solve_update(float* poses, float* patches, int E, int P, int t0, int t1,
     }
     for (int lev = L - 1; lev >= 0; lev--)
       hipLaunchKernelGGL(k_cr_back, dim3(cap((long long)(nl[lev] / 2) * kPanelsR)), dim3(kPT),
-                         kPanelLds, s, lev, w);
+                         kPanelLds2, s, lev, w);
     hipLaunchKernelGGL(k_border_part, dim3(kBP), dim3(256), kPanelLds, s, w);
     hipLaunchKernelGGL(k_border_reduce, dim3(grid_of((long long)kMaxNB6 * (kMaxNB6 + 1))),
                        dim3(kT), 0, s, w);
