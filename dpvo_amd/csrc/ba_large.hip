@@ -740,7 +740,8 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
 #pragma unroll
     for (int q = 0; q < 3; q++) {
       const int i = ty + 32 * p, j = tx + 32 * q;
-      a[p][q] = (i < n && j < n) ? src[(size_t)i * lda + j] : 0.0;
+      const double v = src[(size_t)min(i, n - 1) * lda + min(j, n - 1)];  // unconditional
+      a[p][q] = (i < n && j < n) ? v : 0.0;
     }
   if (tid == 0) bad = 0;
   double* W = vbuf + 24 * kMaxM;  // [6][kMaxM]
@@ -807,7 +808,9 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
       }
     }
     __syncthreads();
-    // (3) update
+    // (3) update, branch-free except for the few waves holding block rows
+    // (padding entries i, j >= n are computed from clamped rows and never
+    // published or stored)
     double wj[3][6];
 #pragma unroll
     for (int q = 0; q < 3; q++) {
@@ -817,8 +820,7 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
     }
 #pragma unroll
     for (int p = 0; p < 3; p++) {
-      const int i = ty + 32 * p;
-      if (i >= n) continue;  // wave-uniform for p = 2
+      const int i = min(ty + 32 * p, n - 1);
       double ci[6];
 #pragma unroll
       for (int u = 0; u < 6; u++) ci[u] = Cw[i * 6 + u];
@@ -830,17 +832,28 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
         a[p][q] = v;
       }
     }
+    // block columns (entry (i, b0 + dc), i outside the block): -V
+    const int ps = (b0 + dr) >> 5, qs = (b0 + dc) >> 5;
+    {
+      double vv[3];
 #pragma unroll
-    for (int p = 0; p < 3; p++) {
-      const int ri = ty + 32 * p - b0;
-      const bool inr = ri >= 0 && ri < 6;
+      for (int p = 0; p < 3; p++) vv[p] = V[min(ty + 32 * p, n - 1) * 6 + min(dc, 5)];
+#pragma unroll
+      for (int p = 0; p < 3; p++)
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+          if (dc < 6 && q == qs && !(dr < 6 && p == ps)) a[p][q] = -vv[p];
+    }
+    // block rows (entry (b0 + dr, j)): W, and P^-1 inside the block
+    if (dr < 6) {
+      const double pv = Pi[dr * 6 + min(dc, 5)];
 #pragma unroll
       for (int q = 0; q < 3; q++) {
-        const int cj = tx + 32 * q - b0;
-        const bool inc = cj >= 0 && cj < 6;
-        if (inr && inc) a[p][q] = Pi[ri * 6 + cj];
-        else if (inr) a[p][q] = W[ri * kMaxM + min(tx + 32 * q, n - 1)];
-        else if (inc) a[p][q] = -V[min(ty + 32 * p, n - 1) * 6 + cj];
+        const double wv = W[dr * kMaxM + min(tx + 32 * q, n - 1)];
+        const double v = (dc < 6 && q == qs) ? pv : wv;
+#pragma unroll
+        for (int p = 0; p < 3; p++)
+          if (p == ps) a[p][q] = v;
       }
     }
   }
@@ -862,16 +875,15 @@ constexpr int kPT = 256;
 // Global -> LDS staging with the loads of 8 elements per thread issued back to
 // back before any is waited on (a plain load/store loop waits once per element:
 // one HBM round trip each).  src(q) gives the value of LDS element q.
+// Every load is unconditional (index clamped into range, value selected
+// afterwards): a conditional load compiles to a branch with its own wait.
 template <typename F>
 __device__ __forceinline__ void stage(double* dst, int total, F src) {
   const int nt = blockDim.x;
   for (int base = threadIdx.x; base < total; base += 8 * nt) {
     double v[8];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int q = base + u * nt;
-      v[u] = q < total ? src(q) : 0.0;
-    }
+    for (int u = 0; u < 8; u++) v[u] = src(min(base + u * nt, total - 1));
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       const int q = base + u * nt;
@@ -885,7 +897,7 @@ __device__ __forceinline__ void stage_a(const double* A, int lda, bool trans, in
                                         double* As) {
   stage(As, M * K, [&](int q) {
     const int r = q / K, k = q - r * K;
-    return trans ? A[(size_t)k * lda + r] : A[(size_t)r * lda + k];
+    return A[trans ? (size_t)k * lda + r : (size_t)r * lda + k];
   });
 }
 // Bs <- columns [c0, c0 + nc) of B (K x *, row-major ldb) or of B^T (B stored
@@ -893,28 +905,32 @@ __device__ __forceinline__ void stage_a(const double* A, int lda, bool trans, in
 __device__ __forceinline__ void stage_b(const double* B, int ldb, bool trans, int K, int c0, int nc,
                                         double* Bs) {
   stage(Bs, K * kPW, [&](int q) {
-    const int k = q / kPW, c = q - k * kPW;
-    double v = 0.0;
-    if (c < nc) v = trans ? B[(size_t)(c0 + c) * ldb + k] : B[(size_t)k * ldb + c0 + c];
-    return v;
+    const int k = q / kPW, c = q - k * kPW, cc = min(c, nc - 1);
+    const double v = B[trans ? (size_t)(c0 + cc) * ldb + k : (size_t)k * ldb + c0 + cc];
+    return c < nc ? v : 0.0;
   });
 }
 // s[a] = sum_k As[r_a][k] Bs[k][tc], r_a = tr + 8 a, k ascending; K even.
+// Branch-free: rows past M read row M - 1 (their sums are never stored); a
+// row guard here compiles to one exec-masked block per row, each waiting on
+// its own LDS read.
 __device__ __forceinline__ void panel_dot(const double* As, int M, int K, const double* Bs,
                                           double s[12]) {
   const int tc = threadIdx.x & (kPW - 1), tr = threadIdx.x >> 5;
-  const int na = (M - tr + 7) >> 3;  // wave-uniform
+  const double* arow[12];
 #pragma unroll
-  for (int a = 0; a < 12; a++) s[a] = 0.0;
+  for (int a = 0; a < 12; a++) {
+    s[a] = 0.0;
+    arow[a] = As + min(tr + 8 * a, M - 1) * K;
+  }
   for (int k = 0; k < K; k += 2) {
     const double b0 = Bs[k * kPW + tc], b1 = Bs[(k + 1) * kPW + tc];
 #pragma unroll
-    for (int a = 0; a < 12; a++)
-      if (a < na) {
-        const double2 av = *reinterpret_cast<const double2*>(As + (tr + 8 * a) * K + k);
-        s[a] += av.x * b0;
-        s[a] += av.y * b1;
-      }
+    for (int a = 0; a < 12; a++) {
+      const double2 av = *reinterpret_cast<const double2*>(arow[a] + k);
+      s[a] += av.x * b0;
+      s[a] += av.y * b1;
+    }
   }
 }
 // C[rows, c0 + tc] = (acc ? C : 0) (+ alpha * s1 if use1) (+ alpha * s2 if use2)
@@ -949,11 +965,13 @@ __device__ void wg_gemm_tn(double* C, int ldc, const double* A, int lda, const d
       __syncthreads();
       stage(As, K * kTM, [&](int q) {
         const int k = q / kTM, i = q % kTM;
-        return (i0 + i < M) ? A[(size_t)k * lda + i0 + i] : 0.0;
+        const double v = A[(size_t)k * lda + min(i0 + i, M - 1)];
+        return (i0 + i < M) ? v : 0.0;
       });
       stage(Bs, K * kTN, [&](int q) {
         const int k = q / kTN, j = q % kTN;
-        return (j0 + j < N) ? B[(size_t)k * ldb + j0 + j] : 0.0;
+        const double v = B[(size_t)k * ldb + min(j0 + j, N - 1)];
+        return (j0 + j < N) ? v : 0.0;
       });
       __syncthreads();
       double s[4][4];

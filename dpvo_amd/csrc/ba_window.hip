@@ -759,12 +759,15 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   for (int u0 = tid; u0 < nuniq; u0 += kB * kWT) {
     unsigned m[kB];
     int p0[kB], p1[kB];
+    // loads are unconditional (index clamped, value selected afterwards): a
+    // guarded load compiles to its own exec branch and wait, one HBM round
+    // trip per item instead of one per batch
 #pragma unroll
     for (int r = 0; r < kB; r++) {
-      const int u = u0 + r * kWT;
-      m[r] = (u < nuniq) ? A.plan.pmask[u] : 0u;
-      p0[r] = (u < nuniq) ? A.plan.poff[u] : 0;
-      p1[r] = (u < nuniq) ? A.plan.poff[u + 1] : 0;
+      const int u = min(u0 + r * kWT, nuniq - 1);
+      m[r] = A.plan.pmask[u];
+      p0[r] = A.plan.poff[u];
+      p1[r] = A.plan.poff[u + 1];
     }
 #pragma unroll
     for (int r = 0; r < kB; r++) {
@@ -835,21 +838,24 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     unsigned msk[kB];
     float cv[kB][4];  // [0][1][1], [1][1][1], [2][1][1], [2][0][0] (ba_cuda.cu:282-285, :225)
 #pragma unroll
-    for (int r = 0; r < kB; r++) {
-      const int u = u0 + r * kWT;
-      const bool live = u < nuniq && cnt[u] != ((u + 1 < nuniq) ? cnt[u + 1] : tot);
-      kx[r] = live ? A.plan.pkk[u] : -1;
-      po[r] = live ? A.plan.poff[u] : 0;
-      msk[r] = live ? A.plan.pmask[u] : 0u;
+    for (int r = 0; r < kB; r++) {  // unconditional loads (see the pass above)
+      const int u = u0 + r * kWT, uc = min(u, nuniq - 1);
+      const bool live = u < nuniq && cnt[uc] != ((uc + 1 < nuniq) ? cnt[uc + 1] : tot);
+      const int k = A.plan.pkk[uc], o = A.plan.poff[uc];
+      const unsigned mm = A.plan.pmask[uc];
+      kx[r] = live ? k : -1;
+      po[r] = live ? o : 0;
+      msk[r] = live ? mm : 0u;
     }
 #pragma unroll
     for (int r = 0; r < kB; r++) {
       const float* pk = A.patches + (size_t)max(kx[r], 0) * 3 * PP;
       const int c11 = P + 1;
-      cv[r][0] = (kx[r] >= 0) ? pk[c11] : 0.f;
-      cv[r][1] = (kx[r] >= 0) ? pk[PP + c11] : 0.f;
-      cv[r][2] = (kx[r] >= 0) ? pk[2 * PP + c11] : 0.f;
-      cv[r][3] = (kx[r] >= 0) ? pk[2 * PP] : 0.f;
+      const float v0 = pk[c11], v1 = pk[PP + c11], v2 = pk[2 * PP + c11], v3 = pk[2 * PP];
+      cv[r][0] = (kx[r] >= 0) ? v0 : 0.f;
+      cv[r][1] = (kx[r] >= 0) ? v1 : 0.f;
+      cv[r][2] = (kx[r] >= 0) ? v2 : 0.f;
+      cv[r][3] = (kx[r] >= 0) ? v3 : 0.f;
     }
 #pragma unroll
     for (int r = 0; r < kB; r++) {
@@ -880,14 +886,10 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   for (int q0 = tid; q0 < nrp; q0 += kB * kWT) {
     int ev[kB];
 #pragma unroll
-    for (int r = 0; r < kB; r++) {
-      const int q = q0 + r * kWT;
-      int e = 0;
-      if (q < nrp) {
-        const int ri = L.rp[q];
-        e = A.plan.epos[rpo[ri] + (q - L.roff[ri])];
-      }
-      ev[r] = e;
+    for (int r = 0; r < kB; r++) {  // unconditional loads (see pass A)
+      const int q = min(q0 + r * kWT, nrp - 1);
+      const int ri = L.rp[q];
+      ev[r] = A.plan.epos[rpo[ri] + (q - L.roff[ri])];
     }
     int64_t gi[kB], gj[kB];
     float2 tg[kB], wt[kB];
@@ -917,9 +919,9 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     for (int r = 0; r < kPr; r++) {
       const int k = tid + r * kWT, sl = k >> 3, c = k & 7;
       const int gp = (sl < N) ? t0w + sl : fmin + (sl - N);
-      pv[r] = (c == 6) ? 1.0f : 0.0f;
-      if (c < 7 && gp >= 0 && gp < A.num_poses && (sl < N || fmin != 0x7fffffff))
-        pv[r] = A.poses[7 * (size_t)gp + c];
+      const bool ok = c < 7 && gp >= 0 && gp < A.num_poses && (sl < N || fmin != 0x7fffffff);
+      const float v = A.poses[7 * (size_t)min(max(gp, 0), A.num_poses - 1) + min(c, 6)];
+      pv[r] = ok ? v : ((c == 6) ? 1.0f : 0.0f);
     }
 #pragma unroll
     for (int r = 0; r < kPr; r++) L.pose[tid + r * kWT] = pv[r];
