@@ -869,9 +869,11 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
   return bad == 0;
 }
 
-// --- one-round-trip panel products (256 threads: tc = tid % 32 column,
-// tr = tid / 32 row group, rows tr + 8 a, a < 12)
-constexpr int kPT = 256;
+// --- one-round-trip panel products (1024 threads: tc = tid % 32 column,
+// tr = tid / 32 row group, rows tr + 32 a, a < kRA)
+constexpr int kPT = 1024;
+constexpr int kRG = kPT / 32;                  // row groups
+constexpr int kRA = (kMaxM + kRG - 1) / kRG;   // rows per thread
 // Global -> LDS staging with the loads of 8 elements per thread issued back to
 // back before any is waited on (a plain load/store loop waits once per element:
 // one HBM round trip each).  src(q) gives the value of LDS element q.
@@ -910,23 +912,23 @@ __device__ __forceinline__ void stage_b(const double* B, int ldb, bool trans, in
     return c < nc ? v : 0.0;
   });
 }
-// s[a] = sum_k As[r_a][k] Bs[k][tc], r_a = tr + 8 a, k ascending; K even.
+// s[a] = sum_k As[r_a][k] Bs[k][tc], r_a = tr + kRG a, k ascending; K even.
 // Branch-free: rows past M read row M - 1 (their sums are never stored); a
 // row guard here compiles to one exec-masked block per row, each waiting on
 // its own LDS read.
 __device__ __forceinline__ void panel_dot(const double* As, int M, int K, const double* Bs,
-                                          double s[12]) {
+                                          double s[kRA]) {
   const int tc = threadIdx.x & (kPW - 1), tr = threadIdx.x >> 5;
-  const double* arow[12];
+  const double* arow[kRA];
 #pragma unroll
-  for (int a = 0; a < 12; a++) {
+  for (int a = 0; a < kRA; a++) {
     s[a] = 0.0;
-    arow[a] = As + min(tr + 8 * a, M - 1) * K;
+    arow[a] = As + min(tr + kRG * a, M - 1) * K;
   }
   for (int k = 0; k < K; k += 2) {
     const double b0 = Bs[k * kPW + tc], b1 = Bs[(k + 1) * kPW + tc];
 #pragma unroll
-    for (int a = 0; a < 12; a++) {
+    for (int a = 0; a < kRA; a++) {
       const double2 av = *reinterpret_cast<const double2*>(arow[a] + k);
       s[a] += av.x * b0;
       s[a] += av.y * b1;
@@ -935,13 +937,13 @@ __device__ __forceinline__ void panel_dot(const double* As, int M, int K, const 
 }
 // C[rows, c0 + tc] = (acc ? C : 0) (+ alpha * s1 if use1) (+ alpha * s2 if use2)
 __device__ __forceinline__ void panel_store(double* C, int ldc, int M, int c0, int nc, double alpha,
-                                            bool acc, const double (&s1)[12], bool use1,
-                                            const double (&s2)[12], bool use2) {
+                                            bool acc, const double (&s1)[kRA], bool use1,
+                                            const double (&s2)[kRA], bool use2) {
   const int tc = threadIdx.x & (kPW - 1), tr = threadIdx.x >> 5;
   if (tc >= nc) return;
 #pragma unroll
-  for (int a = 0; a < 12; a++) {
-    const int r = tr + 8 * a;
+  for (int a = 0; a < kRA; a++) {
+    const int r = tr + kRG * a;
     if (r < M) {
       double* cp = C + (size_t)r * ldc + c0 + tc;
       double v = acc ? *cp : 0.0;
@@ -1074,7 +1076,7 @@ __global__ void __launch_bounds__(kPT) k_cr_mul(int lev, int top, Ws w, const do
     else if (seg == 1) stage_b(Lcur + o * mm, m, true, m, c0, nc, Bs);   // A[o, r] = L[o]^T
     else stage_b(Ro, nr, false, m, c0, nc, Bs);
     __syncthreads();
-    double s[12];
+    double s[kRA];
     panel_dot(As, m, m, Bs, s);
     if (seg == 0) panel_store(w.Y1 + o * mm, m, m, c0, nc, 1.0, false, s, true, s, false);
     else if (seg == 1) panel_store(w.Y2 + o * mm, m, m, c0, nc, 1.0, false, s, true, s, false);
@@ -1106,7 +1108,7 @@ __global__ void __launch_bounds__(kPT) k_cr_b(int lev, Ws w, const double* Lcur,
     const int c0 = pnl * kPW, ncol = seg == 1 ? nr : m;
     if (c0 >= ncol || (seg == 2 && !has_r2) || (!has_l && !has_r)) continue;  // block-uniform
     const int nc = min(kPW, ncol - c0);
-    double s1[12], s2[12];
+    double s1[kRA], s2[kRA];
     __syncthreads();
     if (seg == 2) {
       stage_a(Lcur + orr * mm, m, false, m, m, As);
@@ -1165,7 +1167,7 @@ __global__ void __launch_bounds__(kPT) k_cr_back(int lev, Ws w) {
     if (c0 >= nr) continue;  // block-uniform
     const int nc = min(kPW, nr - c0);
     const int k = 2 * e + 1, o = k * st, l = (k - 1) * st, r = (k + 1) * st;
-    double s1[12], s2[12];
+    double s1[kRA], s2[kRA];
     __syncthreads();
     const bool has_r = k + 1 < n;
     if (has_r && two_fit(m)) {  // one round trip for both products
