@@ -723,12 +723,15 @@ __device__ __forceinline__ double rcp_f64(double p) {
 // n x n matrix src (n = 6 nb <= kMaxM, row stride lda) into dst (row stride n;
 // global or LDS; may alias src: every load happens before the first barrier).
 // 1024 threads; thread (ty, tx) keeps entries (ty + 32 p, tx + 32 q) in
-// registers.  TWO barriers per block step (a scalar Gauss-Jordan needs one per
-// pivot, six per block, each on the pivot's dependency chain): (1) the owners publish the raw block rows Rw (6 x n) and
-// block columns Cw (n x 6) (parity double-buffered); (2) wave 0 inverts the
-// pivot P = A[b, b] (one entry per lane, pivot row / column by shuffles) and
-// forms W = P^-1 Rw and V = Cw P^-1; then every entry outside the block gets
-// a -= Cw_i . W_j (6 FMAs), block rows W, block columns -V, the pivot P^-1.
+// registers.  Three barriers per block step (a scalar Gauss-Jordan needs one
+// per pivot, six per block, each on the pivot's dependency chain): (1) the
+// owners publish the raw block rows Rw (6 x n) and block columns Cw (n x 6)
+// (parity double-buffered); (2a) wave 0 inverts the pivot P = A[b, b] (one
+// entry per lane, pivot row / column by shuffles); (2b) every thread forms one
+// entry of W = P^-1 Rw and of V = Cw P^-1; (3) every entry outside the block
+// gets a -= Cw_i . W_j (6 FMAs), block rows W, block columns -V, the pivot P^-1.
+// W, V, P^-1 are single-buffered: their writers of step K + 1 have passed
+// barrier (1) of K + 1, so every reader of step K is done.
 // vbuf: 2 (Rw + Cw) + W + V + P^-1 = 2 * 12 kMaxM + 12 kMaxM + 36 doubles.
 constexpr size_t kBgjDoubles = 36 * (size_t)kMaxM + 40;
 __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda, double* dst, double* vbuf) {
@@ -773,7 +776,7 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
       }
     }
     __syncthreads();
-    // (2) wave 0: P^-1, W, V
+    // (2a) wave 0: P^-1
     if (tid < kWave) {
       // lane 6 r + c holds P[r][c]; pivot row / column by lane shuffles
       const int lr = min(tid, 35) / 6, lc = min(tid, 35) % 6;
@@ -793,19 +796,20 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
       }
       if (!ok && tid == 0) bad = 1;
       if (tid < 36) Pi[tid] = x;
-      wave_lds_sync();
-      for (int q = tid; q < 6 * n; q += kWave) {
-        const int d = q / n, j = q - d * n;  // W[d][j]
-        const int i = q / 6, e = q - i * 6;  // V[i][e]
-        double sw = 0.0, sv = 0.0;
+    }
+    __syncthreads();
+    // (2b) W = P^-1 Rw and V = Cw P^-1, one entry of each per thread
+    for (int q = tid; q < 6 * n; q += blockDim.x) {
+      const int d = q / n, j = q - d * n;  // W[d][j]
+      const int i = q / 6, e = q - i * 6;  // V[i][e]
+      double sw = 0.0, sv = 0.0;
 #pragma unroll
-        for (int u = 0; u < 6; u++) {
-          sw = fma(Pi[d * 6 + u], Rw[u * kMaxM + j], sw);
-          sv = fma(Cw[i * 6 + u], Pi[u * 6 + e], sv);
-        }
-        W[d * kMaxM + j] = sw;
-        V[i * 6 + e] = sv;
+      for (int u = 0; u < 6; u++) {
+        sw = fma(Pi[d * 6 + u], Rw[u * kMaxM + j], sw);
+        sv = fma(Cw[i * 6 + u], Pi[u * 6 + e], sv);
       }
+      W[d * kMaxM + j] = sw;
+      V[i * 6 + e] = sv;
     }
     __syncthreads();
     // (3) update, branch-free except for the few waves holding block rows
