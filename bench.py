@@ -16,6 +16,11 @@ replay it; each replay leaves a ~8.7 us launch gap).
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
+Without a launcher (WORLD_SIZE unset) and N > 1, bench.py starts the N ranks
+itself (one child process per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+in each child's environment, before anything touches the GPU) and exits with
+the worst child exit code; rank 0 prints the line.
+
 Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 """
 from __future__ import annotations
@@ -77,6 +82,58 @@ def algorithmic_corr_bytes(coords, H2s, W2s, scales, C, p, R, feat_bytes):
     return total, per_level
 
 
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(n, port, base=None):
+    """Environment of each of the n ranks bench.py starts itself (the same
+    variables torch.distributed.run sets)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                  "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                  "MASTER_PORT": str(port), "DPVO_BENCH_CHILD": "1"})
+        # RCCL / CUDA-tensor IPC on this host needs dmabuf (see the environment notes)
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(n, argv, cmd=None):
+    """Run `cmd` (default: this script with `argv`) as n rank processes and
+    return the worst exit code.  Called only when WORLD_SIZE is unset: nothing
+    in this parent process has touched the GPU (no torch import at all)."""
+    import subprocess
+
+    cmd = cmd or [sys.executable, os.path.abspath(__file__), *argv]
+    procs = [subprocess.Popen(cmd, env=e) for e in rank_envs(n, free_port())]
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def warm_until(step_fn, torch, min_ms=200.0, max_steps=100000):
+    """Run steps until at least min_ms of wall time has passed (GPU clocks
+    ramp on a fresh box; a fixed step count can end before they have)."""
+    t0 = time.perf_counter()
+    n = 0
+    while n < max_steps:
+        for _ in range(8):
+            step_fn(n)
+            n += 1
+        torch.cuda.synchronize()
+        if (time.perf_counter() - t0) * 1e3 >= min_ms:
+            break
+    return n
+
+
 def sharded_main(args, torch, dist, world, rank, local, dev):
     """--sharded: BASELINE cfg4 global BA (1024 frames x 96 patches, ~131k
     edges, N = 1023 free poses), edge-sharded by source frame over the ranks
@@ -104,6 +161,7 @@ def sharded_main(args, torch, dist, world, rank, local, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    warm_until(lambda i: step(), torch, args.warm_ms)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -197,12 +255,18 @@ def main():
     ap.add_argument("--features", choices=["f32", "f16"], default="f32",
                     help="feature dtype of the pyramid / gmap rings (f16 = the fork's "
                          "MIXED_PRECISION runtime: A-CORR on v_mfma_f32_16x16x16_f16)")
+    ap.add_argument("--warm-ms", type=float, default=200.0,
+                    help="after the --warmup steps, keep stepping (untimed) until this much wall "
+                         "time has passed: clocks ramp on a fresh box")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured hipGraph (default: launch every kernel "
                          "from Python each step, as DPVO does; the host stays ahead of the GPU, "
                          "while a graph replay leaves a ~8.7 us gap between steps: "
                          "profiles/r02_trace_overlap_vs_inline.txt)")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # --gpus N without a launcher: start the N ranks here (before any GPU call)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
@@ -210,9 +274,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE = {world}")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local)
     if args.sharded:
         return sharded_main(args, torch, dist, world, rank, local, dev)
@@ -296,6 +363,7 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    warm_until(step, torch, args.warm_ms)
     # A-CORR kernel time for the roofline: HIP events around the corr launch
     # (same stream) over eager steps outside the timed region
     n_ev = 20
@@ -327,6 +395,7 @@ def main():
             step(0)
         graph.replay()
         torch.cuda.synchronize()
+        warm_until(lambda i: graph.replay(), torch, args.warm_ms)
 
     if world > 1:
         dist.barrier()
@@ -346,7 +415,12 @@ def main():
     # without a fatal status (raises RuntimeError otherwise)
     ba_status = fastba.cuda_ba.check_status(poses)
 
+    per_rank = [args.steps / elapsed]
     if world > 1:
+        mine = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        allt = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allt, mine)
+        per_rank = [args.steps / t.item() for t in allt]
         t = torch.tensor([elapsed, corr_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, corr_ms = t[0].item(), t[1].item()
@@ -387,8 +461,12 @@ def main():
             "value": value,
             "unit": "update-iterations/s",
             "n_gpus": world,
+            "world_size": dist.get_world_size() if world > 1 else 1,
+            "backend": dist.get_backend() if world > 1 else None,
+            "per_rank_value": per_rank,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warm_ms": args.warm_ms,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
             "scaling": "weak",

@@ -86,16 +86,23 @@ def build(force=False, verbose=False):
     # one object per HIP source (incremental), then one shared library
     objdir = os.path.join(OUT, "obj")
     os.makedirs(objdir, exist_ok=True)
-    objs = []
+    objs, cmds = [], []
     for src in srcs:
         obj = os.path.join(objdir, os.path.basename(src).replace(".hip", ".o"))
         objs.append(obj)
         if force or _stale(obj, [src] + hdr + [__file__]):
-            cmd = [hipcc, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c",
-                   "-fvisibility=hidden", "-mcode-object-version=5", "-Wno-unused-result",
-                   f"-I{INCLUDE}", f'-DDPVO_GIT_REV="{_git_rev()}"',
-                   *SOURCE_FLAGS.get(os.path.basename(src), []), src, "-o", obj]
-            _run(cmd, verbose)
+            cmds.append([hipcc, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c",
+                         "-fvisibility=hidden", "-mcode-object-version=5", "-Wno-unused-result",
+                         f"-I{INCLUDE}", f'-DDPVO_GIT_REV="{_git_rev()}"',
+                         *SOURCE_FLAGS.get(os.path.basename(src), []), src, "-o", obj])
+    # the objects are independent: compile them concurrently (bounded by the
+    # host's share of CPUs; MAX_JOBS is honoured as on the GPU box)
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1)), 16))
+    if cmds:
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(lambda c: _run(c, verbose), cmds))
     if force or _stale(lib, objs):
         cmd = [hipcc, f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-o", lib]
         _run(cmd, verbose)

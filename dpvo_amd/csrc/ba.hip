@@ -43,7 +43,7 @@ constexpr int kMaxFree = 20;  // pose-block masks are 32-bit; lower S blocks of 
 constexpr int kPerThread = kMaxSetupE / kSetupThreads;
 constexpr int kCtlBytes = 512;
 constexpr int kSetupLds = 160 * 1024;
-constexpr int kMarks = 1152;  // [0, 128) phases; window kernel: [128 + 256 it + g] assembled, [640 + 256 it + g] all partials seen
+constexpr int kMarks = 1664;  // [0, 128) phases; window kernel per workgroup: [128 + 256 it + g] assembled, [640 + 256 it + g] all partials seen, [1152 + g] setup, [1408 + g] it 0 pre-reduction
 constexpr int kNoPose = 31;
 constexpr int kEC = 16;  // doubles per position record of E terms
 
@@ -1051,7 +1051,8 @@ bool ba_window_supported(int E, int N, int P);
 int ba_window_launch(float* poses, float* patches, const float* intrinsics, const float* target,
                      const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                      const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
-                     int iterations, char* scratch, int* status, int64_t* marks, void* stream);
+                     int iterations, char* scratch, int* status, int64_t* marks, double* dxo,
+                     void* stream);
 int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int E, int num_patches,
                    int num_poses, int t0, int t1, char* scratch, int* status, void* stream,
                    const int* t0d);
@@ -1071,20 +1072,23 @@ int ba_window_reproject_plan_insert(const float* poses, const float* patches,
 int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
                   const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                   const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
-                  int iterations, char* scratch, int* status, int64_t* marks, void* stream,
-                  const int* t0d);
+                  int iterations, char* scratch, int* status, int64_t* marks, double* dxo,
+                  void* stream, const int* t0d);
 // ba_large.hip: large graphs (global BA, cfg4)
 size_t gba_workspace_bytes(int E, int N);
 int gba_forward(float* poses, float* patches, const float* intrinsics, const float* target,
                 const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                 const int64_t* kk, int E, int P, int num_poses, int num_patches, int PPF, int t0,
                 int t1, int iterations, void* workspace, size_t workspace_bytes, void* stream);
+double* gba_dx(void* workspace, int E, int N);
 
 }  // namespace dpvo
 
 namespace {
 // 0 auto (window), 2 multi-kernel, 4 large-graph path, 5 window (1 / 3 removed)
 int g_ba_path = 0;
+// instrumentation: phase marks stamped by the window kernel (dpvo_ba_set_marks)
+bool g_ba_marks = false;
 }
 
 using namespace dpvo;
@@ -1285,6 +1289,30 @@ DPVO_EXPORT int dpvo_ba_phase_marks(const void* workspace, int E, int t0, int t1
              : DPVO_ERR_LAUNCH;
 }
 
+DPVO_EXPORT int dpvo_ba_set_marks(int on) {
+  g_ba_marks = on != 0;
+  return DPVO_OK;
+}
+
+DPVO_EXPORT int dpvo_ba_last_dx(const void* workspace, int E, int t0, int t1, double* out,
+                                void* stream) {
+  if (!workspace || !out || E <= 0 || t1 < t0) return DPVO_ERR_INVALID;
+  const int N = t1 - t0;
+  if (N == 0) return DPVO_OK;
+  const double* src;
+  if (use_large(E, N)) {
+    src = gba_dx(const_cast<void*>(workspace), E, N);
+  } else {
+    BaWs w;
+    ba_layout(E, N, (char*)workspace, &w);
+    src = w.dX;
+  }
+  return hipMemcpyAsync(out, src, sizeof(double) * 6 * N, hipMemcpyDeviceToDevice,
+                        as_stream(stream)) == hipSuccess
+             ? DPVO_OK
+             : DPVO_ERR_LAUNCH;
+}
+
 // instrumentation: per-workgroup start/end stamps of the last iteration launch
 DPVO_EXPORT int dpvo_ba_workgroup_marks(const void* workspace, int E, int t0, int t1, int64_t* out,
                                         void* stream) {
@@ -1321,7 +1349,8 @@ DPVO_EXPORT int dpvo_ba_forward(float* poses, float* patches, const float* intri
   if ((g_ba_path == 0 || g_ba_path == 5) && ba_window_supported(E, N, P))
     return ba_window_launch(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
                             num_poses, num_patches, t0, t1, iterations,
-                            (char*)workspace + base_bytes, w.meta + 1, w.tmark, stream);
+                            (char*)workspace + base_bytes, w.meta + 1,
+                            g_ba_marks ? w.tmark : nullptr, w.dX, stream);
   ensure_lds_limits();
   hipStream_t s = as_stream(stream);
   BaArgs a = make_args(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
@@ -1386,7 +1415,7 @@ DPVO_EXPORT int dpvo_ba_forward_planned(float* poses, float* patches, const floa
   const size_t base_bytes = ba_layout(E, t1 - t0, (char*)workspace, &w);
   return ba_window_run(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
                        num_poses, num_patches, t0, t1, iterations, (char*)workspace + base_bytes,
-                       w.meta + 1, w.tmark, stream, nullptr);
+                       w.meta + 1, g_ba_marks ? w.tmark : nullptr, w.dX, stream, nullptr);
 }
 
 DPVO_EXPORT int dpvo_ba_forward_planned_dev(float* poses, float* patches, const float* intrinsics,
@@ -1406,7 +1435,7 @@ DPVO_EXPORT int dpvo_ba_forward_planned_dev(float* poses, float* patches, const 
   const size_t base_bytes = ba_layout(E, N, (char*)workspace, &w);
   return ba_window_run(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
                        num_poses, num_patches, 0, N, iterations, (char*)workspace + base_bytes,
-                       w.meta + 1, w.tmark, stream, t0_dev);
+                       w.meta + 1, g_ba_marks ? w.tmark : nullptr, w.dX, stream, t0_dev);
 }
 
 DPVO_EXPORT int dpvo_reproject(const float* poses, const float* patches, const float* intrinsics,

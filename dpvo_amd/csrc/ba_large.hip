@@ -1514,6 +1514,12 @@ int gba_status(const void* workspace, int E, int N, int* out, void* stream) {
   return launch_status();
 }
 
+double* gba_dx(void* workspace, int E, int N) {
+  Ws w;
+  layout(E, N, (char*)workspace, &w);
+  return w.dX;
+}
+
 double* gba_packed(void* workspace, int E, int N) {
   Ws w;
   layout(E, N, (char*)workspace, &w);

@@ -61,6 +61,10 @@ constexpr long long kSpin = 2000000;    // 20 ms of the 100 MHz wall clock
 constexpr int kEpochWord = kWMaxG;      // flags[kWMaxG]: epoch of the last call
 constexpr int kFlagWords = kWMaxG + 8;
 constexpr int kRefine = 1;              // fp64 refinement steps of the solve
+// raw buffer resources (gfx950 dword 3) and the buffer builtins' cache-policy
+// bit for sc1 (agent-coherent: bypasses the CU's L1; stores write through L2)
+constexpr int kBufDword3 = 0x00020000;
+constexpr int kSc1 = 16;
 
 // status bits (shared with the other BA paths; see dpvo_hot.h)
 constexpr int kStChol = 1, kStClamp = 2, kStTimeout = 16, kStCap = 32;
@@ -93,12 +97,18 @@ struct WArgs {
   float* ejg;        // [2][E][12] E entries by edge and iteration parity (fp32), HBM fallback
   int* status;       // [1] OR of status bits (workspace meta)
   int* sink;         // caller's sticky status word (dpvo_ba_set_status_sink) or null
-  int64_t* marks;    // [64] wall-clock stamps of workgroup 0 (may be null)
+  int64_t* marks;    // [1664] wall-clock stamps (instrumentation, dpvo_ba_set_marks): [0, 64)
+                     // phases of workgroup 0, [128 + 256 it + g] / [640 + 256 it + g] per
+                     // workgroup assembled / all partials seen, [1152 + g] setup done,
+                     // [1408 + g] iteration 0 assembled (before the reduction); null on
+                     // product calls
+  double* dxo;       // [6N] dX of the latest iteration (workgroup 0; dpvo_ba_last_dx) or null
   const int* t0d;    // device t0 or null (then t0)
 };
 
 __device__ __forceinline__ size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
 typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 __device__ bool wait_flag(long long* p, long long target) {
   const long long t0 = (long long)wall_clock64();
@@ -484,13 +494,27 @@ struct WL {  // LDS layout of one workgroup
   float* ej;           // [nrp][12] E entries of the last linearisation (LDS), or null
   char* region;        // union: chunk scratch / reduction table / solver
   // E entries of relevant edge q for iteration parity par: in LDS by q, else in
-  // the shared HBM buffer by edge id and parity.  Every workgroup holding an
+  // the shared HBM buffer by edge id and parity (write-through sc1 stores and
+  // sc1 loads there: see assemble).  Every workgroup holding an
   // edge writes the same bits there (identical poses, depths and order), and
   // parity keeps a workgroup one iteration ahead off the slot a slower one
   // still reads (it can reach iteration it + 2 only after every workgroup
   // has published it + 1, i.e. finished reading iteration it's entries)
-  __device__ __forceinline__ float* ej_at(const float* ejg, int E, int q, int par) const {
-    return ej ? ej + 12 * (size_t)q : const_cast<float*>(ejg) + ((size_t)par * E + eid[q]) * 12;
+  __device__ __forceinline__ void ld_ej(const float* ejg, int E, int q, int par, float4& e0,
+                                        float4& e1, float4& e2) const {
+    if (ej) {
+      const float4* e4 = reinterpret_cast<const float4*>(ej + 12 * (size_t)q);
+      e0 = e4[0];
+      e1 = e4[1];
+      e2 = e4[2];
+    } else {  // written sc1 (write-through) by other threads: read past the CU's L1
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(ejg), 0, (int)(sizeof(float) * 24 * (size_t)E), kBufDword3);
+      const int o = (int)(sizeof(float) * 12 * ((size_t)par * E + eid[q]));
+      e0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, kSc1));
+      e1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, 0, kSc1));
+      e2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 32, 0, kSc1));
+    }
   }
 };
 
@@ -572,10 +596,28 @@ __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, do
         uq += (wr * (double)o.r[row]) * (double)o.Jz[row];
       }
       // E entries (fp32) for the depth update after the solve
-      float4* eo = reinterpret_cast<float4*>(L.ej_at(A.ejg, A.E, q, par));
-      eo[0] = make_float4((float)ejv[0], (float)ejv[1], (float)ejv[2], (float)ejv[3]);
-      eo[1] = make_float4((float)ejv[4], (float)ejv[5], (float)eiv[0], (float)eiv[1]);
-      eo[2] = make_float4((float)eiv[2], (float)eiv[3], (float)eiv[4], (float)eiv[5]);
+      {
+        const float4 e0 = make_float4((float)ejv[0], (float)ejv[1], (float)ejv[2], (float)ejv[3]);
+        const float4 e1 = make_float4((float)ejv[4], (float)ejv[5], (float)eiv[0], (float)eiv[1]);
+        const float4 e2 = make_float4((float)eiv[2], (float)eiv[3], (float)eiv[4], (float)eiv[5]);
+        if (L.ej) {
+          float4* eo = reinterpret_cast<float4*>(L.ej + 12 * (size_t)q);
+          eo[0] = e0;
+          eo[1] = e1;
+          eo[2] = e2;
+        } else {
+          // shared HBM buffer: every workgroup holding the edge writes the same
+          // bits; write-through (sc1) stores leave no dirty line in any XCD's
+          // L2, so no stale copy of an earlier same-parity iteration can be
+          // written back over a newer one (the L2s are not coherent)
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+              A.ejg, 0, (int)(sizeof(float) * 24 * (size_t)A.E), kBufDword3);
+          const int o = (int)(sizeof(float) * 12 * ((size_t)par * A.E + L.eid[q]));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, e0), rs, o, 0, kSc1);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, e1), rs, o + 16, 0, kSc1);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, e2), rs, o + 32, 0, kSc1);
+        }
+      }
       double* ps = pe + 14 * (size_t)(q - q0);
       ps[0] = cq;
       ps[1] = uq;
@@ -739,6 +781,27 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     tri_of(t, ta, tb);
     L.tri[t] = (unsigned short)((ta << 8) | tb);
   }
+  // ---------------- setup: relevant patches of this workgroup ----------------
+  // rel(u): mask holds a and b and u % S == sub; workgroup 0 also takes the
+  // patches without a free pose (their dZ = Q u).  One scan packs
+  // (#patches << 16 | #edges) (E <= 4096 keeps both below 2^16).
+  // Global round trips are the setup's cost (~1 us each on a cold L2): the
+  // plan meta and the first kB * 256 patches' plan entries are loaded in ONE
+  // batch (speculatively, indices clamped to the E-sized arrays), then the
+  // patch values, the edge ids and the pose table in a second, then the
+  // per-edge inputs in a third.
+  constexpr int kB = 8;
+  const unsigned need = (NB > 0) ? ((1u << a) | (1u << b)) : 0u;
+  unsigned m0[kB];
+  int pa0[kB], pb0[kB], kx0[kB];
+#pragma unroll
+  for (int r = 0; r < kB; r++) {
+    const int u = min(tid + r * kWT, A.E - 1);
+    m0[r] = A.plan.pmask[u];
+    pa0[r] = A.plan.poff[u];
+    pb0[r] = A.plan.poff[u + 1];
+    kx0[r] = A.plan.pkk[u];
+  }
   const int nuniq = A.plan.meta[0], fmin = A.plan.meta[1];
   if (tid == 0) {
     ctl[cFail] = 0;
@@ -746,22 +809,20 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     ctl[cTimeout] = 0;
     ctl[cCap] = 0;
   }
-
-  // ---------------- setup: relevant patches of this workgroup ----------------
-  // rel(u): mask holds a and b and u % S == sub; workgroup 0 also takes the
-  // patches without a free pose (their dZ = Q u).  One scan packs
-  // (#patches << 16 | #edges) (E <= 4096 keeps both below 2^16).
-  const unsigned need = (NB > 0) ? ((1u << a) | (1u << b)) : 0u;
   int* cnt = (int*)(lds + off);  // [nuniq] scan input / prefix (kept until the records are built)
-  // setup loops load kB items per thread before using any (one global round
-  // trip per kB * 256 items instead of one per 256)
-  constexpr int kB = 8;
-  for (int u0 = tid; u0 < nuniq; u0 += kB * kWT) {
+  auto relevant = [&](unsigned m, int u) {
+    return (NB == 0) ? true : (((m & need) == need && (u % S) == sub) || (g == 0 && m == 0));
+  };
+#pragma unroll
+  for (int r = 0; r < kB; r++) {
+    const int u = tid + r * kWT;
+    if (u < nuniq) cnt[u] = relevant(m0[r], u) ? ((1 << 16) | (pb0[r] - pa0[r])) : 0;
+  }
+  // patches past the first batch (nuniq > kB * 256): loaded here, kB per thread
+  // per round trip (loads unconditional: index clamped, value selected after)
+  for (int u0 = tid + kB * kWT; u0 < nuniq; u0 += kB * kWT) {
     unsigned m[kB];
     int p0[kB], p1[kB];
-    // loads are unconditional (index clamped, value selected afterwards): a
-    // guarded load compiles to its own exec branch and wait, one HBM round
-    // trip per item instead of one per batch
 #pragma unroll
     for (int r = 0; r < kB; r++) {
       const int u = min(u0 + r * kWT, nuniq - 1);
@@ -772,10 +833,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
 #pragma unroll
     for (int r = 0; r < kB; r++) {
       const int u = u0 + r * kWT;
-      if (u >= nuniq) continue;
-      const bool rel = (NB == 0) ? true
-                                 : (((m[r] & need) == need && (u % S) == sub) || (g == 0 && m[r] == 0));
-      cnt[u] = rel ? ((1 << 16) | (p1[r] - p0[r])) : 0;
+      if (u < nuniq) cnt[u] = relevant(m[r], u) ? ((1 << 16) | (p1[r] - p0[r])) : 0;
     }
   }
   __syncthreads();
@@ -821,7 +879,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   L.eid = (int*)take(sizeof(int) * (nrp + 1));
   L.region = take(region_b);
   // target/weight and E entries in LDS when they fit; else E entries in the
-  // shared HBM buffer (WL::ej_at) and target/weight read from the inputs
+  // shared HBM buffer (WL::ld_ej) and target/weight read from the inputs
   const size_t tw_b = sizeof(float4) * (nrp + 1), ej_b = sizeof(float) * 12 * (nrp + 1);
   L.tw = nullptr;
   L.ej = nullptr;
@@ -831,65 +889,135 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   } else if (o2 + tw_b <= (size_t)kWLds) {
     L.tw = (float4*)take(tw_b);
   }
-  // pass A, thread per relevant patch: records, edge offsets, patch of each edge
+  // pass A1, thread per relevant patch, no global loads: record offsets, the
+  // patch of every position, the final-depth writer
   int* rpo = reinterpret_cast<int*>(L.qu);  // first sorted position (until the first linearisation)
-  for (int u0 = tid; u0 < nuniq && nrel > 0; u0 += kB * kWT) {
+  auto record = [&](int u, int kx, int po, unsigned m) {
+    const int c0 = cnt[u], c1 = (u + 1 < nuniq) ? cnt[u + 1] : tot;
+    const int ri = c0 >> 16, q0 = c0 & 0xffff, ne = (c1 - c0) & 0xffff;
+    L.roff[ri] = q0;
+    rpo[ri] = po;
+    for (int t = 0; t < ne; t++) L.rp[q0 + t] = (unsigned short)ri;
+    if (ne > kChunk) ctl[cCap] = 1;
+    // writer of the final depth: the diagonal workgroup of the lowest free
+    // pose with share u % Sd; workgroup 0 for patches without a free pose
+    bool own;
+    if (NB == 0) own = true;
+    else if (m == 0) own = (g == 0);
+    else own = diag && (int)__builtin_ctz(m) == a && (u % A.Sd) == sub;
+    L.pkx[ri] = own ? kx : -1;
+    return ri;
+  };
+  auto live = [&](int u) {
+    return u < nuniq && cnt[u] != ((u + 1 < nuniq) ? cnt[u + 1] : tot);
+  };
+  bool lv0[kB];
+#pragma unroll
+  for (int r = 0; r < kB; r++) {
+    const int u = tid + r * kWT;
+    lv0[r] = nrel > 0 && live(min(u, nuniq - 1)) && u < nuniq;
+    if (lv0[r]) record(u, kx0[r], pa0[r], m0[r]);
+  }
+  for (int u0 = tid + kB * kWT; u0 < nuniq && nrel > 0; u0 += kB * kWT) {
     int kx[kB], po[kB];
     unsigned msk[kB];
-    float cv[kB][4];  // [0][1][1], [1][1][1], [2][1][1], [2][0][0] (ba_cuda.cu:282-285, :225)
 #pragma unroll
-    for (int r = 0; r < kB; r++) {  // unconditional loads (see the pass above)
-      const int u = u0 + r * kWT, uc = min(u, nuniq - 1);
-      const bool live = u < nuniq && cnt[uc] != ((uc + 1 < nuniq) ? cnt[uc + 1] : tot);
-      const int k = A.plan.pkk[uc], o = A.plan.poff[uc];
-      const unsigned mm = A.plan.pmask[uc];
-      kx[r] = live ? k : -1;
-      po[r] = live ? o : 0;
-      msk[r] = live ? mm : 0u;
+    for (int r = 0; r < kB; r++) {
+      const int uc = min(u0 + r * kWT, nuniq - 1);
+      kx[r] = A.plan.pkk[uc];
+      po[r] = A.plan.poff[uc];
+      msk[r] = A.plan.pmask[uc];
     }
 #pragma unroll
     for (int r = 0; r < kB; r++) {
-      const float* pk = A.patches + (size_t)max(kx[r], 0) * 3 * PP;
-      const int c11 = P + 1;
-      const float v0 = pk[c11], v1 = pk[PP + c11], v2 = pk[2 * PP + c11], v3 = pk[2 * PP];
-      cv[r][0] = (kx[r] >= 0) ? v0 : 0.f;
-      cv[r][1] = (kx[r] >= 0) ? v1 : 0.f;
-      cv[r][2] = (kx[r] >= 0) ? v2 : 0.f;
-      cv[r][3] = (kx[r] >= 0) ? v3 : 0.f;
-    }
-#pragma unroll
-    for (int r = 0; r < kB; r++) {
-      if (kx[r] < 0) continue;
       const int u = u0 + r * kWT;
-      const int c0 = cnt[u], c1 = (u + 1 < nuniq) ? cnt[u + 1] : tot;
-      const int ri = c0 >> 16, q0 = c0 & 0xffff, ne = (c1 - c0) & 0xffff;
-      L.roff[ri] = q0;
-      rpo[ri] = po[r];
-      for (int t = 0; t < ne; t++) L.rp[q0 + t] = (unsigned short)ri;
-      if (ne > kChunk) ctl[cCap] = 1;
-      L.nxy[ri] = make_float2((cv[r][0] - cx) / fx, (cv[r][1] - cy) / fy);
-      L.dep[ri] = cv[r][2];
-      L.dbase[ri] = cv[r][3];  // patch_retr_kernel reads [2][0][0] (:225)
-      // writer of the final depth: the diagonal workgroup of the lowest free
-      // pose with share u % Sd; workgroup 0 for patches without a free pose
-      const unsigned m = msk[r];
-      bool own;
-      if (NB == 0) own = true;
-      else if (m == 0) own = (g == 0);
-      else own = diag && (int)__builtin_ctz(m) == a && (u % A.Sd) == sub;
-      L.pkx[ri] = own ? kx[r] : -1;
+      if (u < nuniq && live(u)) record(u, kx[r], po[r], msk[r]);
     }
   }
   if (tid == 0) L.roff[nrel] = nrp;
   __syncthreads();
-  // pass B, thread per relevant edge: slots, edge index, target/weight
+  // pass A2 + pass B, second round trip: the values of this thread's first-batch
+  // patches, the edge ids of its first kB relevant edges and the pose table,
+  // all issued before any is used
+  // patch values: [0][1][1], [1][1][1], [2][1][1], [2][0][0] (ba_cuda.cu:282-285, :225)
+  float cv[kB][4];
+  const int c11 = P + 1;
+#pragma unroll
+  for (int r = 0; r < kB; r++) {
+    const float* pk = A.patches + (size_t)(lv0[r] ? kx0[r] : 0) * 3 * PP;
+    cv[r][0] = pk[c11];
+    cv[r][1] = pk[PP + c11];
+    cv[r][2] = pk[2 * PP + c11];
+    cv[r][3] = pk[2 * PP];
+  }
+  int ev0[kB];
+#pragma unroll
+  for (int r = 0; r < kB; r++) {
+    const int q = min(tid + r * kWT, max(nrp - 1, 0));
+    const int ri = nrp > 0 ? L.rp[q] : 0;
+    const int p = nrp > 0 ? rpo[ri] + (q - L.roff[ri]) : 0;
+    ev0[r] = A.plan.epos[min(max(p, 0), A.E - 1)];
+  }
+  // pose table: free poses t0.., then fixed ones from fmin
+  constexpr int kPr = kWSlots * 8 / kWT;
+  float pv[kPr];
+#pragma unroll
+  for (int r = 0; r < kPr; r++) {
+    const int k = tid + r * kWT, sl = k >> 3, c = k & 7;
+    const int gp = (sl < N) ? t0w + sl : fmin + (sl - N);
+    pv[r] = A.poses[7 * (size_t)min(max(gp, 0), A.num_poses - 1) + min(c, 6)];
+  }
+  auto patch_vals = [&](int u, const float* v) {
+    const int ri = cnt[u] >> 16;
+    L.nxy[ri] = make_float2((v[0] - cx) / fx, (v[1] - cy) / fy);
+    L.dep[ri] = v[2];
+    L.dbase[ri] = v[3];  // patch_retr_kernel reads [2][0][0] (:225)
+  };
+#pragma unroll
+  for (int r = 0; r < kB; r++)
+    if (lv0[r]) patch_vals(tid + r * kWT, cv[r]);
+#pragma unroll
+  for (int r = 0; r < kPr; r++) {
+    const int k = tid + r * kWT, sl = k >> 3, c = k & 7;
+    const int gp = (sl < N) ? t0w + sl : fmin + (sl - N);
+    const bool ok = c < 7 && gp >= 0 && gp < A.num_poses && (sl < N || fmin != 0x7fffffff);
+    L.pose[k] = ok ? pv[r] : ((c == 6) ? 1.0f : 0.0f);
+  }
+  // patches past the first batch
+  for (int u0 = tid + kB * kWT; u0 < nuniq && nrel > 0; u0 += kB * kWT) {
+    float cw[kB][4];
+    int kx[kB];
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      const int u = u0 + r * kWT, uc = min(u, nuniq - 1);
+      kx[r] = (u < nuniq && live(uc)) ? A.plan.pkk[uc] : -1;
+    }
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      const float* pk = A.patches + (size_t)max(kx[r], 0) * 3 * PP;
+      cw[r][0] = pk[c11];
+      cw[r][1] = pk[PP + c11];
+      cw[r][2] = pk[2 * PP + c11];
+      cw[r][3] = pk[2 * PP];
+    }
+#pragma unroll
+    for (int r = 0; r < kB; r++)
+      if (kx[r] >= 0) patch_vals(u0 + r * kWT, cw[r]);
+  }
+  // pass B, thread per relevant edge: slots, edge index, target/weight (the
+  // third round trip; further batches of kB edges per thread each need two)
   for (int q0 = tid; q0 < nrp; q0 += kB * kWT) {
     int ev[kB];
+    if (q0 == tid) {
 #pragma unroll
-    for (int r = 0; r < kB; r++) {  // unconditional loads (see pass A)
-      const int q = min(q0 + r * kWT, nrp - 1);
-      const int ri = L.rp[q];
-      ev[r] = A.plan.epos[rpo[ri] + (q - L.roff[ri])];
+      for (int r = 0; r < kB; r++) ev[r] = ev0[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < kB; r++) {  // unconditional loads (see above)
+        const int q = min(q0 + r * kWT, nrp - 1);
+        const int ri = L.rp[q];
+        ev[r] = A.plan.epos[rpo[ri] + (q - L.roff[ri])];
+      }
     }
     int64_t gi[kB], gj[kB];
     float2 tg[kB], wt[kB];
@@ -911,23 +1039,9 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       if (L.tw) L.tw[q] = make_float4(tg[r].x, tg[r].y, wt[r].x, wt[r].y);
     }
   }
-  // pose table: free poses t0.., then fixed ones from fmin
-  {
-    constexpr int kPr = kWSlots * 8 / kWT;
-    float pv[kPr];
-#pragma unroll
-    for (int r = 0; r < kPr; r++) {
-      const int k = tid + r * kWT, sl = k >> 3, c = k & 7;
-      const int gp = (sl < N) ? t0w + sl : fmin + (sl - N);
-      const bool ok = c < 7 && gp >= 0 && gp < A.num_poses && (sl < N || fmin != 0x7fffffff);
-      const float v = A.poses[7 * (size_t)min(max(gp, 0), A.num_poses - 1) + min(c, 6)];
-      pv[r] = ok ? v : ((c == 6) ? 1.0f : 0.0f);
-    }
-#pragma unroll
-    for (int r = 0; r < kPr; r++) L.pose[tid + r * kWT] = pv[r];
-  }
   __syncthreads();
   mark(A, 1);
+  if (A.marks && tid == 0 && g < 256) A.marks[1152 + g] = (int64_t)wall_clock64();  // setup done
   const int nrel_e = nrel;
 
   // ---------------- iterations ----------------
@@ -952,8 +1066,8 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
         for (int q = L.roff[ri]; q < L.roff[ri + 1]; q++) {
           const unsigned c = L.ec[q];
           const unsigned si = c & 0xff, sj = c >> 8;
-          const float4* e4 = reinterpret_cast<const float4*>(L.ej_at(A.ejg, A.E, q, (it - 1) & 1));
-          const float4 e0 = e4[0], e1 = e4[1], e2 = e4[2];
+          float4 e0, e1, e2;
+          L.ld_ej(A.ejg, A.E, q, (it - 1) & 1, e0, e1, e2);
           if (sj < (unsigned)N) {
             const double* d = L.dX + 6 * sj;
             ex += (double)e0.x * d[0] + (double)e0.y * d[1] + (double)e0.z * d[2] +
@@ -986,9 +1100,12 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       assemble<0>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
     } else if (diag) {
       assemble<1>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
+      mark(A, mb + 4);
+      if (A.marks && tid == 0 && it == 0 && g < 256) A.marks[1408 + g] = (int64_t)wall_clock64();
       reduce_acc<27>(acc, red, part);
     } else {
       assemble<2>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
+      if (A.marks && tid == 0 && it == 0 && g < 256) A.marks[1408 + g] = (int64_t)wall_clock64();
       reduce_acc<36>(acc, red, part);
     }
     mark(A, mb + 0);
@@ -1054,22 +1171,25 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     }
 #else
     {
-      // the kPart / 2 used 16-B pairs of every slot as 16-B sc1 loads (inline
-      // asm: no builtin emits a 16-B sc1 load), kIn in flight per thread and
-      // drained by one explicit wait before any use: one round for G <= 256
+      // the kPart / 2 used 16-B pairs of every slot as 16-B sc1 buffer loads
+      // (the builtin's cache-policy bit 4 is sc1 on gfx950; the compiler tracks
+      // them, so its own waits cover every use), kIn in flight per thread: one
+      // round for G <= 256
       constexpr int kHalfPart = kPart / 2;
       static_assert(kPart % 2 == 0 && kPartPad % 2 == 0, "16-B pairs");
       const int tot_p = kHalfPart * A.G;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          pbuf, 0, (int)(sizeof(double) * kPartPad * A.G), kBufDword3);
       constexpr int kIn = 12;
       for (int t0_ = tid; t0_ < tot_p; t0_ += kIn * kWT) {
         f64x2 v[kIn];
 #pragma unroll
         for (int r = 0; r < kIn; r++) {
           const int t = min(t0_ + r * kWT, tot_p - 1), sl = t / kHalfPart, k = t - sl * kHalfPart;
-          const double* src = pbuf + (size_t)sl * kPartPad + 2 * k;
-          asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[r]) : "v"(src) : "memory");
+          v[r] = __builtin_bit_cast(
+              f64x2, __builtin_amdgcn_raw_buffer_load_b128(
+                         rs, (int)(sizeof(double) * ((size_t)sl * kPartPad + 2 * k)), 0, kSc1));
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
         for (int r = 0; r < kIn; r++) {
           const int t = t0_ + r * kWT, sl = t / kHalfPart, k = t - sl * kHalfPart;
@@ -1116,7 +1236,11 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     sv.v1 = sv.v0 + 6 * N;
     const bool ok = wsolve(sv, N, kRefine, &ctl[cFail]);
     const bool zero = !ok || ctl[cTimeout] != 0;
-    for (int k = tid; k < 6 * N; k += kWT) L.dX[k] = zero ? 0.0 : sv.x[k];  // (dpvo/ba.py:17-21)
+    for (int k = tid; k < 6 * N; k += kWT) {
+      const double v = zero ? 0.0 : sv.x[k];  // (dpvo/ba.py:17-21)
+      L.dX[k] = v;
+      if (g == 0 && A.dxo) A.dxo[k] = v;
+    }
     if (!ok && tid == 0) ctl[cFailAny] = 1;
     __syncthreads();
     mark(A, mb + 3);
@@ -1142,8 +1266,8 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       for (int q = L.roff[ri]; q < L.roff[ri + 1]; q++) {
         const unsigned c = L.ec[q];
         const unsigned si = c & 0xff, sj = c >> 8;
-        const float4* e4 = reinterpret_cast<const float4*>(L.ej_at(A.ejg, A.E, q, (it - 1) & 1));
-        const float4 e0 = e4[0], e1 = e4[1], e2 = e4[2];
+        float4 e0, e1, e2;
+        L.ld_ej(A.ejg, A.E, q, (it - 1) & 1, e0, e1, e2);
         if (sj < (unsigned)N) {
           const double* d = L.dX + 6 * sj;
           ex += (double)e0.x * d[0] + (double)e0.y * d[1] + (double)e0.z * d[2] +
@@ -1456,25 +1580,27 @@ int ba_window_reproject_plan_insert(const float* poses, const float* patches,
 int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
                   const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                   const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
-                  int iterations, char* scratch, int* status, int64_t* marks, void* stream,
-                  const int* t0d = nullptr);
+                  int iterations, char* scratch, int* status, int64_t* marks, double* dxo,
+                  void* stream, const int* t0d = nullptr);
 
 int ba_window_launch(float* poses, float* patches, const float* intrinsics, const float* target,
                      const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                      const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
-                     int iterations, char* scratch, int* status, int64_t* marks, void* stream) {
+                     int iterations, char* scratch, int* status, int64_t* marks, double* dxo,
+                     void* stream) {
   const int rc = ba_window_plan(ii, jj, kk, E, num_patches, num_poses, t0, t1, scratch, status,
                                 stream, nullptr);
   if (rc) return rc;
   return ba_window_run(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, E, P,
-                       num_poses, num_patches, t0, t1, iterations, scratch, status, marks, stream);
+                       num_poses, num_patches, t0, t1, iterations, scratch, status, marks, dxo,
+                       stream);
 }
 
 int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
                   const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                   const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
-                  int iterations, char* scratch, int* status, int64_t* marks, void* stream,
-                  const int* t0d) {
+                  int iterations, char* scratch, int* status, int64_t* marks, double* dxo,
+                  void* stream, const int* t0d) {
   set_attrs();
   if (iterations > 63) return DPVO_ERR_UNSUPPORTED;  // 6-bit iteration tag per epoch
   const int N = t1 - t0;
@@ -1514,6 +1640,7 @@ int ba_window_run(float* poses, float* patches, const float* intrinsics, const f
   a.status = status;
   a.sink = a.plan.sink;
   a.marks = marks;
+  a.dxo = dxo;
   hipLaunchKernelGGL(ba_window_kernel, dim3(w.G), dim3(kWT), kWLds, st, a);
   return launch_status();
 }

@@ -253,17 +253,26 @@ void ba_forward_planned(torch::Tensor ws, torch::Tensor poses, torch::Tensor pat
   track_status(ws, poses, E, t0, t1);
 }
 
-// Same call; returns the 1152 phase marks (100 MHz ticks: [0, 128) phases; window kernel
-// [128 + 256 it + g] / [640 + 256 it + g] per-workgroup assembled / partials seen) followed by
-// the multi-kernel path's per-workgroup marks.
+// Same call; returns the 1664 phase marks (100 MHz ticks: [0, 128) phases; window kernel
+// [128 + 256 it + g] / [640 + 256 it + g] per-workgroup assembled / partials seen, [1152 + g]
+// setup done, [1408 + g] iteration 0 assembled before its reduction) followed by the
+// multi-kernel path's per-workgroup marks.
 torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
                                torch::Tensor intrinsics, torch::Tensor target, torch::Tensor weight,
                                torch::Tensor lmbda, torch::Tensor ii, torch::Tensor jj,
                                torch::Tensor kk, int PPF, int t0, int t1, int iterations,
                                bool eff_impl) {
-  auto ws = ba_forward_ws(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, PPF, t0,
-                          t1, iterations, eff_impl);
-  auto out = torch::zeros({1152}, poses.options().dtype(torch::kInt64));
+  check_status(dpvo_ba_set_marks(1), "cuda_ba.forward_marks");
+  torch::Tensor ws;
+  try {
+    ws = ba_forward_ws(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, PPF, t0, t1,
+                       iterations, eff_impl);
+  } catch (...) {
+    dpvo_ba_set_marks(0);
+    throw;
+  }
+  check_status(dpvo_ba_set_marks(0), "cuda_ba.forward_marks");
+  auto out = torch::zeros({1664}, poses.options().dtype(torch::kInt64));
   if (!ws.defined()) return out;
   check_status(dpvo_ba_phase_marks(ws.data_ptr(), ii.numel(), t0, t1, out.data_ptr<int64_t>(),
                                    current_stream()),
@@ -275,6 +284,34 @@ torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
                                        current_stream()),
                "cuda_ba.forward_marks");
   return torch::cat({out, wg});
+}
+
+// Same call; returns the pose step dX [N, 6] (fp64) of the last iteration
+// (ba_cuda.cu:561-562) -- the parity tests' view of the solve.
+torch::Tensor ba_forward_dx(torch::Tensor poses, torch::Tensor patches, torch::Tensor intrinsics,
+                            torch::Tensor target, torch::Tensor weight, torch::Tensor lmbda,
+                            torch::Tensor ii, torch::Tensor jj, torch::Tensor kk, int PPF, int t0,
+                            int t1, int iterations, bool eff_impl) {
+  auto ws = ba_forward_ws(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, PPF, t0,
+                          t1, iterations, eff_impl);
+  const int N = t1 > t0 ? t1 - t0 : 0;
+  auto out = torch::zeros({N, 6}, poses.options().dtype(torch::kFloat64));
+  if (!ws.defined() || N == 0) return out;
+  check_status(dpvo_ba_last_dx(ws.data_ptr(), ii.numel(), t0, t1, out.data_ptr<double>(),
+                               current_stream()),
+               "cuda_ba.forward_dx");
+  return out;
+}
+
+// dX [N, 6] of the last iteration of forward_planned(_dev) on workspace ws
+torch::Tensor ba_last_dx(torch::Tensor ws, int64_t E, int t0, int t1) {
+  const int N = t1 > t0 ? t1 - t0 : 0;
+  auto out = torch::zeros({N, 6}, ws.options().dtype(torch::kFloat64));
+  if (N == 0) return out;
+  check_status(dpvo_ba_last_dx(ws.data_ptr(), (int)E, t0, t1, out.data_ptr<double>(),
+                               current_stream()),
+               "cuda_ba.last_dx");
+  return out;
 }
 
 // ba.cpp:47-53 -> cuda_reproject (ba_cuda.cu:585-616)
@@ -893,7 +930,8 @@ void kf_shift(torch::Tensor kf, int64_t M, torch::Tensor st, torch::Tensor ii, t
     cap = (int)(delta_log->numel() / 7);
   }
   check_status(dpvo_kf_shift(dev_scalar(kf, "kf"), (int)M, const_cast<int32_t*>(dev_scalar(st, "st")),
-                             L(ii), L(jj), L(kk), dev_scalar(counts, "counts"), (int)ii.numel(),
+                             L(ii), L(jj), L(kk), const_cast<int32_t*>(dev_scalar(counts, "counts")),
+                             (int)ii.numel(),
                              ptrs.data(), bytes.data(), ring.data(), (int)ptrs.size(), pp, ts, dl,
                              dt, dc, cap, current_stream()),
                "cuda_ba.kf_shift");
@@ -905,8 +943,12 @@ void edges_loop(torch::Tensor poses, torch::Tensor patches, torch::Tensor intrin
                 c10::optional<torch::Tensor> last_global_ba, int64_t removal_window,
                 int64_t max_edge_age, int64_t global_opt_freq, int64_t keyframe_index,
                 double backend_thresh, int64_t max_num_edges, int64_t nms, torch::Tensor work,
-                torch::Tensor out_kk, torch::Tensor out_jj, torch::Tensor out_n) {
+                torch::Tensor out_kk, torch::Tensor out_jj, torch::Tensor out_n,
+                c10::optional<torch::Tensor> errors) {
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(poses.device());
+  int32_t* err = (errors && errors->defined())
+                     ? const_cast<int32_t*>(dev_scalar(*errors, "errors"))
+                     : nullptr;
   TORCH_CHECK(work.scalar_type() == torch::kFloat32 &&
                   work.numel() >= (int64_t)dpvo_edges_loop_work_floats(),
               "work: float32[edges_loop_work_floats()]");
@@ -924,7 +966,7 @@ void edges_loop(torch::Tensor poses, torch::Tensor patches, torch::Tensor intrin
                                (int)keyframe_index, (float)backend_thresh, (int)max_num_edges,
                                (int)nms, work.data_ptr<float>(), out_kk.data_ptr<int64_t>(),
                                out_jj.data_ptr<int64_t>(),
-                               const_cast<int32_t*>(dev_scalar(out_n, "out_n")),
+                               const_cast<int32_t*>(dev_scalar(out_n, "out_n")), err,
                                current_stream()),
                "cuda_ba.edges_loop");
 }
@@ -957,6 +999,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gba_solve_update", &gba_solve_update, "large-graph BA: solve + retraction");
   m.def("gba_info", &gba_info, "status, nuniq, nitems, nblk, nI, nB, g, nsb (device int32[8])");
   m.def("forward_marks", &ba_forward_marks, "forward + per-phase wall-clock marks");
+  m.def("forward_dx", &ba_forward_dx, "forward; returns the last iteration's dX [N, 6] (fp64)");
+  m.def("last_dx", &ba_last_dx, "dX [N, 6] of the last iteration of a planned forward on ws");
   m.def("reproject_ordered_plan", &ba_reproject_ordered_plan,
         "reproject + A-CORR edge order + BA plan (workspace for forward_planned), one launch");
   m.def("reproject_ordered_plan_dev", &ba_reproject_ordered_plan_dev,

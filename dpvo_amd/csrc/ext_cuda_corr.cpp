@@ -18,7 +18,6 @@ std::vector<torch::Tensor> corr_forward(torch::Tensor fmap1, torch::Tensor fmap2
   TORCH_CHECK(coords.size(2) == 2, "coords must be [B,M,2,H,W]");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(fmap1.device());
   fmap1 = fmap1.contiguous();
-  fmap2 = fmap2.contiguous();
   coords = coords.contiguous();
   ii = idx64(ii, "ii");
   jj = idx64(jj, "jj");
@@ -26,6 +25,27 @@ std::vector<torch::Tensor> corr_forward(torch::Tensor fmap1, torch::Tensor fmap2
   TORCH_CHECK(ii.numel() >= M && jj.numel() >= M, "ii/jj shorter than coords.size(1)");
   TORCH_CHECK(fmap1.size(3) == H && fmap1.size(4) == W, "fmap1 patch size != coords size");
   const int Dp = 2 * radius + 1;
+  // a channels-last level ([B,N,C,H,W] view of [B,N,H,W,C] memory, e.g. a
+  // DPVO pyramid allocated channels-last) takes the
+  // matrix-core path as a one-level forward_levels (fp32 accumulation; the
+  // result is returned in the fmap dtype, as the reference does) instead of
+  // a transposing .contiguous() copy of the whole ring
+  if (fmap2.permute({0, 1, 3, 4, 2}).is_contiguous() && fmap2.size(2) > 1) {
+    auto o32 = torch::empty({B, M, Dp, Dp, H, W, 1}, fmap1.options().dtype(torch::kFloat32));
+    const void* f2p = fmap2.data_ptr();
+    const int H2 = fmap2.size(3), W2 = fmap2.size(4);
+    const float one = 1.0f;
+    const int st = dpvo_corr_forward_levels_nhwc(
+        fmap1.data_ptr(), &f2p, &H2, &W2, &one, 1, coords.data_ptr<float>(),
+        ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), B, M, fmap1.size(2), H, W, fmap1.size(1),
+        fmap2.size(1), radius, dtype_code(fmap1), o32.data_ptr<float>(), current_stream());
+    if (st != DPVO_ERR_UNSUPPORTED) {
+      check_status(st, "cuda_corr.forward");
+      auto o = o32.view({B, M, Dp, Dp, H, W});
+      return {fmap1.scalar_type() == torch::kFloat32 ? o : o.to(fmap1.scalar_type())};
+    }
+  }
+  fmap2 = fmap2.contiguous();
   auto out = torch::empty({B, M, Dp, Dp, H, W}, fmap1.options());
   check_status(dpvo_corr_forward(fmap1.data_ptr(), fmap2.data_ptr(), coords.data_ptr<float>(),
                                  ii.data_ptr<int64_t>(), jj.data_ptr<int64_t>(), B, M,

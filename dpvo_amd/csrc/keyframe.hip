@@ -142,6 +142,9 @@ __device__ __forceinline__ float flow_px(const float* Pi, const float* Pj, const
 #pragma clang fp contract(fast)
 
 constexpr int kKfT = 256;
+// PatchGraph error flags (counts[2], dpvo_amd/patchgraph.py DevicePatchGraph.errors)
+constexpr int kPgErrLoopCap = 4;    // edges_loop: device frame count above n_cap, no loop edges
+constexpr int kPgErrDeltaFull = 8;  // kf_shift: pg.delta log full, a record was not kept
 
 // ---- DPVO.keyframe: motion magnitude and decision (dpvo.py:586-599, 619-624) ----
 // st = {n, m} (device frame counters).  motionmag(a, b) = mean over the P x P
@@ -215,11 +218,15 @@ __global__ void __launch_bounds__(kKfT) kf_motion_kernel(
 // a device log of (t1, t0, dP) records; runs before the frame shift
 __global__ void kf_delta_kernel(const int* __restrict__ kf, const float* __restrict__ poses,
                                 const int64_t* __restrict__ tstamps, float* __restrict__ dlog,
-                                int64_t* __restrict__ tlog, int* __restrict__ dcnt, int cap) {
+                                int64_t* __restrict__ tlog, int* __restrict__ dcnt, int cap,
+                                int* __restrict__ errors) {
   if (threadIdx.x != 0 || blockIdx.x != 0 || !kf[0]) return;
   const int k = kf[1];
   const int slot = *dcnt;
-  if (slot >= cap) return;
+  if (slot >= cap) {  // the record would be lost (the reference dict never drops one): flag it
+    atomicOr(errors, kPgErrDeltaFull);
+    return;
+  }
   const G7 dp = g_mul(g_load(poses + 7 * k), g_store_load(g_inv(g_load(poses + 7 * (k - 1)))));
   for (int c = 0; c < 3; c++) dlog[7 * slot + c] = dp.t[c];
   for (int c = 0; c < 4; c++) dlog[7 * slot + 3 + c] = dp.q[c];
@@ -298,13 +305,17 @@ __global__ void kf_decrement_kernel(int* __restrict__ st, const int* __restrict_
 // (patches[..., 1, 1]).  Group value: sum(flow * valid) / max(count, 1) in
 // fp32 if count > 0.75 M else inf.
 struct LoopCfg {
-  int P, M, rw, age, gof, ki, nj;
+  int P, M, rw, age, gof, ki, nj, n_cap;
   float thresh;
   int max_edges, nms;
 };
 
 __device__ __forceinline__ bool loop_window(const LoopCfg& c, int n, const int* last_ba, int& j0,
                                             int& lo, int& nf) {
+  // the launch (group grid, sort size, suppression bitmap) was sized for
+  // n <= n_cap: a larger device frame count takes no loop edges (the caller
+  // sees error bit 4, see dpvo_edges_loop)
+  if (n > c.n_cap) return false;
   if (last_ba && n - last_ba[0] < c.gof) return false;  // dpvo.py:984
   const int l = n - c.rw;
   if (l <= 0) return false;  // patchgraph.py:70-71
@@ -361,7 +372,7 @@ constexpr int kElMaxOut = 1024;
 __global__ void __launch_bounds__(kElT) el_select_kernel(
     const float* __restrict__ gflow, const int* __restrict__ gi, const int* __restrict__ st,
     int* __restrict__ last_ba, LoopCfg c, int64_t* __restrict__ out_kk,
-    int64_t* __restrict__ out_jj, int* __restrict__ out_n) {
+    int64_t* __restrict__ out_jj, int* __restrict__ out_n, int* __restrict__ errors) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   unsigned long long* keys = reinterpret_cast<unsigned long long*>(lds);
   unsigned* bits = reinterpret_cast<unsigned*>(keys + kElSort);
@@ -371,7 +382,10 @@ __global__ void __launch_bounds__(kElT) el_select_kernel(
   const int n = st[0];
   int j0, lo, nf;
   if (!loop_window(c, n, last_ba, j0, lo, nf)) {
-    if (tid == 0) *out_n = 0;
+    if (tid == 0) {
+      *out_n = 0;
+      if (n > c.n_cap && errors) atomicOr(errors, kPgErrLoopCap);
+    }
     return;
   }
   const int ng = c.nj * nf;
@@ -469,7 +483,7 @@ DPVO_EXPORT int dpvo_kf_motion(const int64_t* ii, const int64_t* jj, const int64
 }
 
 DPVO_EXPORT int dpvo_kf_shift(const int32_t* kf, int M, int32_t* st, int64_t* ii, int64_t* jj,
-                              int64_t* kk, const int32_t* counts, int max_edges,
+                              int64_t* kk, int32_t* counts, int max_edges,
                               void* const* frame_arrays, const int64_t* bytes_per_frame,
                               const int32_t* ring, int narrays, const float* poses,
                               const int64_t* tstamps, float* delta_log, int64_t* delta_tstamps,
@@ -494,7 +508,7 @@ DPVO_EXPORT int dpvo_kf_shift(const int32_t* kf, int M, int32_t* st, int64_t* ii
   sa.count = narrays;
   if (log)
     hipLaunchKernelGGL(kf_delta_kernel, dim3(1), dim3(64), 0, s, (const int*)kf, poses, tstamps,
-                       delta_log, delta_tstamps, (int*)delta_count, delta_cap);
+                       delta_log, delta_tstamps, (int*)delta_count, delta_cap, (int*)counts + 2);
   const int eg = (int)std::min<long long>((max_edges + 255) / 256, 1024);
   hipLaunchKernelGGL(kf_shift_edges_kernel, dim3(eg), dim3(256), 0, s, ii, jj, kk,
                      (const int*)counts, (const int*)kf, M);
@@ -512,7 +526,7 @@ DPVO_EXPORT int dpvo_edges_loop(const float* poses, const float* patches, const 
                                 int32_t* last_global_ba, int removal_window, int max_edge_age,
                                 int global_opt_freq, int keyframe_index, float backend_thresh,
                                 int max_num_edges, int nms, float* work, int64_t* out_kk,
-                                int64_t* out_jj, int32_t* out_n, void* stream) {
+                                int64_t* out_jj, int32_t* out_n, int32_t* errors, void* stream) {
   if (!poses || !patches || !intrinsics || !ix || !st || !work || !out_kk || !out_jj || !out_n ||
       P < 2 || M <= 0 || n_cap < 0 || removal_window < 0 || max_edge_age < 0 || nms < 0 ||
       max_num_edges < 0)
@@ -528,6 +542,7 @@ DPVO_EXPORT int dpvo_edges_loop(const float* poses, const float* patches, const 
   c.thresh = backend_thresh;
   c.max_edges = max_num_edges;
   c.nms = nms;
+  c.n_cap = n_cap;
   const int nf_cap = std::min(std::max(n_cap - removal_window, 0), max_edge_age);
   const long long ng_cap = (long long)c.nj * nf_cap;
   // sort size, suppression bitmap (n_cap x nj bits) and the accepted-edge list
@@ -549,7 +564,7 @@ DPVO_EXPORT int dpvo_edges_loop(const float* poses, const float* patches, const 
                                                (int)lds) == hipSuccess;
   if (!attr) return DPVO_ERR_LAUNCH;
   hipLaunchKernelGGL(el_select_kernel, dim3(1), dim3(kElT), lds, s, gflow, gi, (const int*)st,
-                     (int*)last_global_ba, c, out_kk, out_jj, (int*)out_n);
+                     (int*)last_global_ba, c, out_kk, out_jj, (int*)out_n, (int*)errors);
   return launch_status();
 }
 

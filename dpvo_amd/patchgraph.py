@@ -69,7 +69,9 @@ class DevicePatchGraph:
     @property
     def errors(self) -> int:
         """1: an append overflowed MAX_EDGES (edges not added); 2: the inactive
-        store was full (removed edges not stored).  Synchronises."""
+        store was full (removed edges not stored); 4: edges_loop saw a frame
+        count above its n_cap (no loop edges taken); 8: the keyframe pg.delta
+        log was full (a record was not kept).  Synchronises."""
         return int(self.counts[2].item())
 
     def append_factors(self, ix, kk, jj):
@@ -178,7 +180,7 @@ class DevicePatchGraph:
                              last_global_ba,
                              int(removal_window), int(max_edge_age), int(global_opt_freq),
                              int(keyframe_index), float(backend_thresh), int(max_num_edges),
-                             int(nms), work, kk, jj, cnt)
+                             int(nms), work, kk, jj, cnt, self.counts[2:3])
         return kk, jj, cnt
 
 

@@ -330,10 +330,11 @@ class UpdateHarness:
 
     def check(self):
         """Raise on a recorded device-side failure (synchronises): an append
-        past MAX_EDGES (error flag 1) or a fatal BA status.  A full inactive
-        store (flag 2) only drops the removed edges, as the reference's
-        warning does (dpvo.py:547-549)."""
-        if self.pg.errors & 1:
+        past MAX_EDGES (error flag 1), an edges_loop frame count past its
+        n_cap (4), a full pg.delta log (8) or a fatal BA status.  A full
+        inactive store (flag 2) only drops the removed edges, as the
+        reference's warning does (dpvo.py:547-549)."""
+        if self.pg.errors & (1 | 4 | 8):
             raise RuntimeError(f"patch graph error flags {self.pg.errors}")
         return fastba.cuda_ba.check_status(self.poses)
 

@@ -262,7 +262,7 @@ int dpvo_ba_status_accumulate(const void* workspace, int E, int t0, int t1, int*
    window-path kernels OR their status into it directly (no extra launch per
    call); dpvo_ba_status_accumulate is then a no-op for that path. */
 int dpvo_ba_set_status_sink(int* acc);
-/* Instrumentation (no reference counterpart): the 128 marks the last
+/* Instrumentation (no reference counterpart): the marks the last
    dpvo_ba_forward on this workspace stamped -- wall clock (100 MHz): [0]
    start, [1] setup, then linearize, patch, schur, solve, update per iteration;
    shader clock: [38] start, [39] end; [40..] finer stamps inside the setup
@@ -272,6 +272,16 @@ int dpvo_ba_phase_marks(const void* workspace, int E, int t0, int t1, int64_t* o
    last Schur launch, [2 x N(N+1)/2] int64 to DEVICE `out`. */
 int dpvo_ba_workgroup_marks(const void* workspace, int E, int t0, int t1, int64_t* out,
                             void* stream);
+/* Instrumentation: when `on` is nonzero the BA kernels of later calls on this
+   process stamp the phase marks above (off by default: the product calls
+   store no marks). */
+int dpvo_ba_set_marks(int on);
+/* Diagnostics (no reference counterpart; the parity tests' view of the
+   reference's dX = chol_solve(S, y), ba_cuda.cu:561-562): the pose step dX
+   [6N] (fp64, pose t0 + i at [6 i .. 6 i + 5]) of the LAST iteration of the
+   last dpvo_ba_forward / dpvo_ba_forward_planned on this workspace, any
+   path, copied to the DEVICE array `out`. */
+int dpvo_ba_last_dx(const void* workspace, int E, int t0, int t1, double* out, void* stream);
 
 /* F-BA on large graphs (ba_large.hip): DPVO's global BA (dpvo.py:695-715 ->
    fastba.BA(..., eff_impl=True), block_e.cu:43-300) and the edge-sharded
@@ -465,9 +475,11 @@ int dpvo_kf_motion(const int64_t* ii, const int64_t* jj, const int64_t* kk, cons
    delta_tstamps[2 x cap] at *delta_count (optional: all three null), shift the
    active edges past k (kk -= M, ii -= 1; jj -= 1), move the per-frame rows
    k+1 .. n-1 of every frame array one row down (ring[a] > 0: row = frame %
-   ring[a], the imap/gmap/fmap rings), then n -= 1, m -= M. */
+   ring[a], the imap/gmap/fmap rings), then n -= 1, m -= M.  A drop whose
+   pg.delta record finds the log full ORs 8 into counts[2] (the patch graph's
+   error word; the record is not kept). */
 int dpvo_kf_shift(const int32_t* kf, int M, int32_t* st, int64_t* ii, int64_t* jj, int64_t* kk,
-                  const int32_t* counts, int max_edges, void* const* frame_arrays,
+                  int32_t* counts, int max_edges, void* const* frame_arrays,
                   const int64_t* bytes_per_frame, const int32_t* ring, int narrays,
                   const float* poses, const int64_t* tstamps, float* delta_log,
                   int64_t* delta_tstamps, int32_t* delta_count, int delta_cap, void* stream);
@@ -480,13 +492,14 @@ int dpvo_kf_shift(const int32_t* kf, int M, int32_t* st, int64_t* ii, int64_t* j
    dpvo_pg_append_dev.  work: dpvo_edges_loop_work_floats() floats.
    Limits: (global_opt_freq - keyframe_index) x min(n_cap - removal_window,
    max_edge_age) <= 16384, n_cap x (global_opt_freq - keyframe_index) <=
-   131072, max_num_edges <= 1024. */
+   131072, max_num_edges <= 1024.  A device n above n_cap takes no loop edges
+   and ORs 4 into *errors (optional; the patch graph's counts[2]). */
 int dpvo_edges_loop(const float* poses, const float* patches, const float* intrinsics,
                     const int64_t* ix, int P, int M, const int32_t* st, int n_cap,
                     int32_t* last_global_ba, int removal_window, int max_edge_age,
                     int global_opt_freq, int keyframe_index, float backend_thresh,
                     int max_num_edges, int nms, float* work, int64_t* out_kk, int64_t* out_jj,
-                    int32_t* out_n, void* stream);
+                    int32_t* out_n, int32_t* errors, void* stream);
 size_t dpvo_edges_loop_work_floats(void);
 
 #ifdef __cplusplus

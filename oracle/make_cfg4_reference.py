@@ -4,7 +4,8 @@ iteration, for tests/test_ba_large_gpu.py::test_cfg4_full_size_matches_oracle.
 
 The oracle (oracle/dpvo_oracle.c, ba_cuda.cu semantics with a dense fp64 S and
 Cholesky) takes minutes at this size, so it runs here once and the committed
-fixture holds only its outputs plus a digest of the inputs; the test rebuilds
+fixture holds only its outputs (poses, inverse depths, the pose step dX)
+plus a digest of the inputs; the test rebuilds
 the inputs from the same seed (dpvo_amd.synthetic, torch CPU generator) and
 checks the digest before comparing.
 
@@ -37,12 +38,14 @@ def main():
     G = synthetic.make_config("cfg4", seed=0)
     t0, t1 = 1, G.F
     t = time.time()
-    P, K = oracle.ba(G.poses.numpy(), G.patches.numpy(), G.intrinsics.numpy(), G.target.numpy(),
-                     G.weight.numpy(), 1e-4, G.ii.numpy(), G.jj.numpy(), G.kk.numpy(), t0, t1, 1)
+    P, K, d = oracle.ba(G.poses.numpy(), G.patches.numpy(), G.intrinsics.numpy(),
+                        G.target.numpy(), G.weight.numpy(), 1e-4, G.ii.numpy(), G.jj.numpy(),
+                        G.kk.numpy(), t0, t1, 1, diagnostics=True)
     dt = time.time() - t
     out = os.path.join(REPO, "tests", "golden", "cfg4_ba1.npz")
     np.savez_compressed(out, poses=P.astype(np.float32), depth=K[:, 2, 1, 1].astype(np.float32),
-                        depth00=K[:, 2, 0, 0].astype(np.float32), digest=digest(G), t0=t0, t1=t1,
+                        depth00=K[:, 2, 0, 0].astype(np.float32), dX=d["dX"].astype(np.float64),
+                        digest=digest(G), t0=t0, t1=t1,
                         E=G.E, seconds=dt)
     print("cfg4 oracle, 1 iteration:", round(dt, 1), "s, E", G.E, "->", out)
 

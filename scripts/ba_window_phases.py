@@ -46,7 +46,8 @@ for rep in range(40):
     prev = 1
     for it in range(iters):
         mb = 2 + 8 * it
-        d[f"it{it}: (apply+) assemble+reduce"] = (m[mb] - m[prev]) * 0.01
+        d[f"it{it}: (apply+) assemble"] = (m[mb + 4] - m[prev]) * 0.01
+        d[f"it{it}: reduce + publish"] = (m[mb] - m[mb + 4]) * 0.01
         d[f"it{it}: wait partials"] = (m[mb + 1] - m[mb]) * 0.01
         d[f"it{it}: gather"] = (m[mb + 2] - m[mb + 1]) * 0.01
         d[f"it{it}: solve"] = (m[mb + 3] - m[mb + 2]) * 0.01
@@ -61,7 +62,7 @@ for k, v in acc.items():
 
 # per-workgroup spread (window kernel stamps [128 + 256 it + g] assembled,
 # [640 + 256 it + g] every partial seen), last call
-if m[128] and len(m) >= 1152:
+if m[128] and len(m) >= 1664:
     import statistics
 
     G = sum(1 for g in range(256) if m[128 + g])
@@ -72,3 +73,11 @@ if m[128] and len(m) >= 1152:
         print(f"it{it}: {G} workgroups assembled at {min(asm):.2f}..{max(asm):.2f} us "
               f"(median {statistics.median(asm):.2f}); all partials seen at "
               f"{min(seen):.2f}..{max(seen):.2f} us; slowest workgroups {order[-5:]}")
+    setup = [(m[1152 + g] - m[0]) * 0.01 for g in range(G)]
+    pre = [(m[1408 + g] - m[0]) * 0.01 for g in range(G)]
+    print(f"setup done at {min(setup):.2f}..{max(setup):.2f} us (median "
+          f"{statistics.median(setup):.2f}); it0 pre-reduction at {min(pre):.2f}..{max(pre):.2f} "
+          f"(median {statistics.median(pre):.2f})")
+    print("per workgroup (g: setup, pre-reduce, assembled, seen):",
+          [(g, round(setup[g], 2), round(pre[g], 2), round((m[128 + g] - m[0]) * 0.01, 2),
+            round((m[640 + g] - m[0]) * 0.01, 2)) for g in order[-8:]])

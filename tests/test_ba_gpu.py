@@ -11,6 +11,7 @@ import pytest
 import torch
 
 import oracle
+from conftest import REL_TOL, assert_ba_rel, rel_err
 from dpvo_amd import synthetic
 
 pytestmark = pytest.mark.gpu
@@ -53,7 +54,13 @@ def _run_oracle(G, t0, t1, iters, diag=False):
                      iters, diagnostics=diag)
 
 
-def _check(P, K, Pr, Kr):
+def _check(P, K, Pr, Kr, G=None, t0=0, t1=0):
+    if G is not None:  # north_star's 1e-4 relative bar on the deltas (conftest.assert_ba_rel)
+        P0, K0 = G.poses.numpy(), G.patches.numpy()
+        if t1 > t0:
+            assert_ba_rel(P, K, Pr, Kr, P0, K0, t0, t1)
+        else:
+            assert rel_err(K[:, 2] - K0[:, 2], Kr[:, 2] - K0[:, 2]) <= REL_TOL
     np.testing.assert_allclose(P, Pr, rtol=0, atol=2e-5)
     np.testing.assert_allclose(K[:, 2], Kr[:, 2], rtol=1e-4, atol=1e-5)
     np.testing.assert_array_equal(K[:, :2], Kr[:, :2])  # x, y never change
@@ -65,7 +72,7 @@ def test_ba_matches_oracle(cb, gpu, path, cfg, iters):
     t1 = G.F
     P, K = _run_gpu(cb, G, gpu, 1, t1, iters)
     Pr, Kr = _run_oracle(G, 1, t1, iters)
-    _check(P, K, Pr, Kr)
+    _check(P, K, Pr, Kr, G, 1, t1)
 
 
 def test_pose_deltas_relative(cb, gpu):
@@ -139,7 +146,7 @@ def test_structure_only(cb, gpu, path):
     G = synthetic.make_config("cfg1", seed=5)
     P, K = _run_gpu(cb, G, gpu, 3, 3, 2)
     Pr, Kr = _run_oracle(G, 3, 3, 2)
-    _check(P, K, Pr, Kr)
+    _check(P, K, Pr, Kr, G, 3, 3)
     np.testing.assert_array_equal(P, G.poses.numpy())
 
 
@@ -148,7 +155,7 @@ def test_window_with_fixed_poses_and_buffers(cb, gpu, path):
     G = synthetic.make_config("cfg2", seed=6, num_poses=64, num_patches=12 * 96 + 500)
     P, K = _run_gpu(cb, G, gpu, 4, 12, 2)
     Pr, Kr = _run_oracle(G, 4, 12, 2)
-    _check(P, K, Pr, Kr)
+    _check(P, K, Pr, Kr, G, 4, 12)
     np.testing.assert_array_equal(P[:4], G.poses.numpy()[:4])
     np.testing.assert_array_equal(P[12:], G.poses.numpy()[12:])
 
@@ -160,7 +167,7 @@ def test_unsorted_edges_and_shuffled_kk(cb, gpu, path):
         setattr(G, k, getattr(G, k)[perm].contiguous())
     P, K = _run_gpu(cb, G, gpu, 1, G.F, 2)
     Pr, Kr = _run_oracle(G, 1, G.F, 2)
-    _check(P, K, Pr, Kr)
+    _check(P, K, Pr, Kr, G, 1, G.F)
 
 
 def test_failed_factorisation_gives_zero_step(cb, gpu):
@@ -229,7 +236,7 @@ def test_fastba_python_surface(gpu):
     fastba.BA(poses, patches, D.intrinsics, D.target, D.weight, torch.tensor([1e-4], device=gpu),
               D.ii, D.jj, D.kk, 1, G.F, M=G.M, iterations=2, eff_impl=False)
     Pr, Kr = _run_oracle(G, 1, G.F, 2)
-    _check(poses.cpu().numpy(), patches.cpu().numpy(), Pr, Kr)
+    _check(poses.cpu().numpy(), patches.cpu().numpy(), Pr, Kr, G, 1, G.F)
 
 
 @pytest.mark.parametrize("seed", [20, 21])
@@ -252,7 +259,7 @@ def test_fused_general_graph_structure(cb, gpu, path, seed):
     G.target, G.weight = tg.contiguous(), wt.contiguous()
     P, K = _run_gpu(cb, G, gpu, 2, G.F - 1, 2)
     Pr, Kr = _run_oracle(G, 2, G.F - 1, 2)
-    _check(P, K, Pr, Kr)
+    _check(P, K, Pr, Kr, G, 2, G.F - 1)
 
 
 def test_window_solve_precision(cb, gpu):
@@ -263,5 +270,5 @@ def test_window_solve_precision(cb, gpu):
         G = synthetic.make_config("cfg2", seed=seed)
         P, K = _run_gpu(cb, G, gpu, 1, G.F, 2)
         Pr, Kr = _run_oracle(G, 1, G.F, 2)
-        _check(P, K, Pr, Kr)
+        _check(P, K, Pr, Kr, G, 1, G.F)
         np.testing.assert_allclose(P, Pr, rtol=0, atol=2e-6)

@@ -12,6 +12,7 @@ import pytest
 import torch
 
 import oracle
+from conftest import REL_TOL, assert_ba_rel, rel_err
 from dpvo_amd import synthetic
 
 pytestmark = pytest.mark.gpu
@@ -39,7 +40,13 @@ def _gpu(cb, G, gpu, t0, t1, iters, eff=True):
     return poses.cpu().numpy(), patches.cpu().numpy()
 
 
-def _check(P, K, Pr, Kr):
+def _check(P, K, Pr, Kr, G=None, t0=0, t1=0):
+    if G is not None:  # north_star's 1e-4 relative bar on the deltas (conftest.assert_ba_rel)
+        P0, K0 = G.poses.numpy(), G.patches.numpy()
+        if t1 > t0:
+            assert_ba_rel(P, K, Pr, Kr, P0, K0, t0, t1)
+        else:
+            assert rel_err(K[:, 2] - K0[:, 2], Kr[:, 2] - K0[:, 2]) <= REL_TOL
     np.testing.assert_allclose(P, Pr, rtol=0, atol=2e-5)
     np.testing.assert_allclose(K[:, 2], Kr[:, 2], rtol=1e-4, atol=1e-5)
     np.testing.assert_array_equal(K[:, :2], Kr[:, :2])
@@ -56,7 +63,7 @@ def test_large_matches_oracle(cb, gpu, cfg, iters):
     G = synthetic.make_config(cfg, seed=1)
     P, K = _gpu(cb, G, gpu, 1, G.F, iters)
     Pr, Kr = _oracle(G, 1, G.F, iters)
-    _check(P, K, Pr, Kr)
+    _check(P, K, Pr, Kr, G, 1, G.F)
 
 
 def test_large_structure_has_border_and_band(cb, gpu):
@@ -78,18 +85,18 @@ def test_forced_large_path_on_window_graph(cb, gpu):
     finally:
         cb.select_path(0)
     Pr, Kr = _oracle(G, 1, G.F, 2)
-    _check(P, K, Pr, Kr)
+    _check(P, K, Pr, Kr, G, 1, G.F)
 
 
 def test_large_fixed_prefix_and_structure_only(cb, gpu):
     G = synthetic.make_config("cfg4s", seed=4)
     P, K = _gpu(cb, G, gpu, 30, G.F, 1)  # poses < 30 fixed
     Pr, Kr = _oracle(G, 30, G.F, 1)
-    _check(P, K, Pr, Kr)
+    _check(P, K, Pr, Kr, G, 30, G.F)
     np.testing.assert_array_equal(P[:30], G.poses.numpy()[:30])
     P, K = _gpu(cb, G, gpu, 5, 5, 2)  # structure only (t0 == t1)
     Pr, Kr = _oracle(G, 5, 5, 2)
-    _check(P, K, Pr, Kr)
+    _check(P, K, Pr, Kr, G, 5, 5)
 
 
 def test_large_is_deterministic(cb, gpu):
@@ -179,7 +186,7 @@ def test_cfg4_full_size_matches_oracle(cb, gpu):
     tests (poses 2e-5 abs, inverse depths 1e-4 rel + 1e-5)."""
     import hashlib
 
-    from conftest import golden
+    from conftest import REL_TOL, golden, rel_err
 
     g = golden("cfg4_ba1")
     G = synthetic.make_config("cfg4", seed=0)
@@ -187,8 +194,19 @@ def test_cfg4_full_size_matches_oracle(cb, gpu):
     for a in (G.poses, G.patches, G.intrinsics, G.ii, G.jj, G.kk, G.target, G.weight):
         h.update(np.ascontiguousarray(a.numpy()).tobytes())
     assert h.hexdigest() == str(g["digest"]), "cfg4 inputs differ from the fixture's"
-    P, K = _gpu(cb, G, gpu, int(g["t0"]), int(g["t1"]), 1)
+    t0, t1 = int(g["t0"]), int(g["t1"])
+    D = G.to(gpu)
+    poses, patches = D.poses.clone(), D.patches.clone()
+    dX = cb.forward_dx(poses, patches, D.intrinsics, D.target, D.weight,
+                       torch.tensor([1e-4], device=gpu), D.ii, D.jj, D.kk, G.M, t0, t1, 1, True)
+    P, K = poses.cpu().numpy(), patches.cpu().numpy()
     assert cb.check_status(torch.zeros(1, device=gpu)) == 0
+    # north_star's bar: pose delta and last-iteration dX within 1e-4 relative
+    P0 = G.poses.numpy()
+    assert rel_err(P[t0:t1] - P0[t0:t1], g["poses"][t0:t1] - P0[t0:t1]) <= REL_TOL
+    assert rel_err(dX.cpu().numpy(), g["dX"]) <= REL_TOL
+    dZr = g["depth"] - G.patches.numpy()[:, 2, 1, 1]
+    assert rel_err(K[:, 2, 1, 1] - G.patches.numpy()[:, 2, 1, 1], dZr) <= REL_TOL
     np.testing.assert_allclose(P, g["poses"], rtol=0, atol=2e-5)
     np.testing.assert_allclose(K[:, 2, 1, 1], g["depth"], rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(K[:, 2, 0, 0], g["depth00"], rtol=1e-4, atol=1e-5)

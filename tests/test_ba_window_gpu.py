@@ -6,12 +6,15 @@ frames with PATCH_LIFETIME 13; M = 10 / 18 / 25 patches per frame give
 E = 3940 / 7092 / 9850 edges (MAX_EDGES = 10000, dpvo/config.py:42).  The BA
 runs as DPVO's local call does: t0 = n - OPTIMIZATION_WINDOW (10), t1 = n
 (dpvo.py:818-824), so edges into the 12 fixed poses take part.
-Tolerances as tests/test_ba_gpu.py (poses 2e-5 abs, inverse depths 1e-4 rel)."""
+Tolerances: north_star's 1e-4 relative bar on the pose delta, the
+inverse-depth delta and the last iteration's pose step dX
+(conftest.assert_ba_rel), plus poses 2e-5 abs, inverse depths 1e-4 rel."""
 import numpy as np
 import pytest
 import torch
 
 import oracle
+from conftest import assert_ba_rel
 from dpvo_amd import synthetic
 
 pytestmark = pytest.mark.gpu
@@ -26,12 +29,13 @@ def cb(gpu):
     return m
 
 
-def _run(cb, G, gpu, t0, t1, iters, lm=1e-4):
+def _run(cb, G, gpu, t0, t1, iters, lm=1e-4, dx=False):
     D = G.to(gpu)
     poses, patches = D.poses.clone(), D.patches.clone()
-    cb.forward(poses, patches, D.intrinsics, D.target, D.weight, torch.tensor([lm], device=gpu),
-               D.ii, D.jj, D.kk, G.M, t0, t1, iters, False)
-    return poses, patches
+    fn = cb.forward_dx if dx else cb.forward
+    d = fn(poses, patches, D.intrinsics, D.target, D.weight, torch.tensor([lm], device=gpu),
+           D.ii, D.jj, D.kk, G.M, t0, t1, iters, False)
+    return (poses, patches, d) if dx else (poses, patches)
 
 
 @pytest.mark.parametrize("M", [10, 18, 25])
@@ -40,17 +44,69 @@ def test_dpvo_window_matches_oracle(cb, gpu, M, iters):
     G = synthetic.make_dpvo_window(M=M, seed=M)
     n = G.F
     t0, t1 = n - 10, n
-    P, K = _run(cb, G, gpu, t0, t1, iters)
+    P, K, dX = _run(cb, G, gpu, t0, t1, iters, dx=True)
     assert cb.check_status(P) == 0
-    Pr, Kr = oracle.ba(G.poses.numpy(), G.patches.numpy(), G.intrinsics.numpy(), G.target.numpy(),
-                       G.weight.numpy(), 1e-4, G.ii.numpy(), G.jj.numpy(), G.kk.numpy(), t0, t1,
-                       iters)
+    Pr, Kr, d = oracle.ba(G.poses.numpy(), G.patches.numpy(), G.intrinsics.numpy(),
+                          G.target.numpy(), G.weight.numpy(), 1e-4, G.ii.numpy(), G.jj.numpy(),
+                          G.kk.numpy(), t0, t1, iters, diagnostics=True)
     P, K = P.cpu().numpy(), K.cpu().numpy()
+    assert_ba_rel(P, K, Pr, Kr, G.poses.numpy(), G.patches.numpy(), t0, t1, dX.cpu().numpy(),
+                  d["dX"])
     np.testing.assert_allclose(P, Pr, rtol=0, atol=2e-5)
     np.testing.assert_allclose(K[:, 2], Kr[:, 2], rtol=1e-4, atol=1e-5)
     np.testing.assert_array_equal(P[:t0], G.poses.numpy()[:t0])  # fixed poses untouched
     # the window moved: the step is not trivially zero
     assert np.abs(P[t0:] - G.poses.numpy()[t0:]).max() > 1e-5
+
+
+def test_dpvo_window_four_iterations_hbm_entries(cb, gpu):
+    """E = 9850 keeps the per-edge E entries in the shared HBM buffer
+    (double-buffered by iteration parity): four iterations reuse each parity
+    slot twice, against the oracle at the 1e-4 relative bar."""
+    G = synthetic.make_dpvo_window(M=25, seed=25)
+    t0, t1 = G.F - 10, G.F
+    P, K = _run(cb, G, gpu, t0, t1, 4)
+    assert cb.check_status(P) == 0
+    Pr, Kr = oracle.ba(G.poses.numpy(), G.patches.numpy(), G.intrinsics.numpy(), G.target.numpy(),
+                       G.weight.numpy(), 1e-4, G.ii.numpy(), G.jj.numpy(), G.kk.numpy(), t0, t1, 4)
+    assert_ba_rel(P.cpu().numpy(), K.cpu().numpy(), Pr, Kr, G.poses.numpy(), G.patches.numpy(),
+                  t0, t1)
+
+
+@pytest.mark.parametrize("iters", [1, 2])
+@pytest.mark.parametrize("features", [torch.float32, torch.float16])
+def test_bench_call_matches_oracle_rel(cb, gpu, iters, features):
+    """The exact call sequence bench.py times on cfg2: the fused frame
+    insertion + reprojection + A-CORR edge order + BA plan launch, then
+    BA(plan=ws), against the oracle at north_star's 1e-4 relative bar (pose
+    delta, inverse-depth delta, last-iteration dX)."""
+    from dpvo_amd import altcorr, fastba
+
+    G = synthetic.make_config("cfg2", seed=0)
+    D = G.to(gpu)
+    t0, t1, mem, levels = 1, G.F, 36, (1, 2, 4, 8)
+    pyr_nchw = synthetic.make_features(mem=mem, C=128, levels=levels, seed=0, device=gpu,
+                                       dtype=features)
+    pyr = [synthetic.channels_last(p) for p in pyr_nchw]
+    poses, patches = D.poses.clone(), D.patches.clone()
+    lm = torch.tensor([1e-4], device=gpu)
+    assert fastba.cuda_ba.plan_supported(G.E, t0, t1, 3)
+    coords, order, ws = fastba.reproject(
+        poses, patches, D.intrinsics, D.ii, D.jj, D.kk, mem=mem, plan_window=(t0, t1),
+        insert=(pyr_nchw[0][0, 3], [p[0, 3] for p in pyr], levels))
+    altcorr.corr_levels(torch.zeros(1, mem * G.M, 128, 3, 3, device=gpu, dtype=features), pyr,
+                        coords, D.kk % (G.M * mem), D.jj % mem, 3, [float(s) for s in levels],
+                        order=order)
+    fastba.BA(poses, patches, D.intrinsics, D.target, D.weight, lm, D.ii, D.jj, D.kk, t0, t1,
+              M=G.M, iterations=iters, plan=ws)
+    dX = cb.last_dx(ws, G.E, t0, t1).cpu().numpy()
+    assert cb.check_status(poses) == 0
+    Pr, Kr, d = oracle.ba(G.poses.numpy(), G.patches.numpy(), G.intrinsics.numpy(),
+                          G.target.numpy(), G.weight.numpy(), 1e-4, G.ii.numpy(), G.jj.numpy(),
+                          G.kk.numpy(), t0, t1, iters, diagnostics=True)
+    e = assert_ba_rel(poses.cpu().numpy(), patches.cpu().numpy(), Pr, Kr, G.poses.numpy(),
+                      G.patches.numpy(), t0, t1, dX, d["dX"])
+    assert e["dP"] < 1e-5  # measured: 0 (1 iteration) / 4.2e-6 (2 iterations)
 
 
 @pytest.mark.parametrize("cfg", ["cfg1", "cfg2"])

@@ -224,6 +224,30 @@ def test_channels_last_equals_nchw_path(cc, gpu):
     assert err <= 1e-5 * max(1.0, a.abs().max().item()), err
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_forward_channels_last_level_matches_oracle(cc, gpu, dtype):
+    """cuda_corr.forward (the reference's per-level entry, dpvo.py:462-465)
+    on a channels-last level -- a DPVO pyramid allocated channels-last
+     -- takes the matrix-core kernel and returns the
+    reference's [B, M, 7, 7, p, p] in the fmap dtype."""
+    from dpvo_amd import synthetic
+
+    f1, f2, co, ii, jj, R = _case(13, M=150, C=128, H2=40, W2=48)
+    if dtype == torch.float16:  # compare on the fp16-rounded inputs
+        f1 = f1.astype(np.float16).astype(np.float32)
+        f2 = f2.astype(np.float16).astype(np.float32)
+    lv = synthetic.channels_last(_t(f2, gpu, dtype))
+    assert not lv.is_contiguous()
+    out, = cc.forward(_t(f1, gpu, dtype), lv, _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R)
+    assert out.dtype == dtype and out.shape == (1, len(ii), 2 * R + 1, 2 * R + 1, 3, 3)
+    ref = oracle.corr_fwd(f1, f2, co, ii, jj, R)
+    _close(out.float().cpu().numpy(), ref, 1e-5 if dtype == torch.float32 else 2e-3)
+    # the NCHW (VALU) path on the same level agrees
+    if dtype == torch.float32:
+        nchw, = cc.forward(_t(f1, gpu), _t(f2, gpu), _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R)
+        _close(out.cpu().numpy(), nchw.cpu().numpy(), 1e-5)
+
+
 def test_to_channels_last_frame_slot(gpu):
     from dpvo_amd import altcorr, synthetic
 

@@ -172,6 +172,51 @@ def test_edges_loop_matches_restatement(gpu, M, n, thresh):
     np.testing.assert_array_equal(pg.ii[:c].cpu().numpy(), ix[rk])
 
 
+def test_edges_loop_frame_count_above_n_cap_is_flagged(gpu):
+    """A device frame count above the n_cap the launch was sized for takes no
+    loop edges and sets patch-graph error bit 4 (the sort and suppression
+    bitmap are sized from n_cap); within n_cap the same graph finds edges."""
+    from dpvo_amd.patchgraph import DevicePatchGraph
+
+    rng = np.random.default_rng(11)
+    M, n, P = 10, 120, 3
+    N = n + 8
+    poses, pts, intr = _loop_scene(rng, N, M, P, n)
+    ix = np.repeat(np.arange(N), M).astype(np.int64)
+    pg = DevicePatchGraph(max_edges=20000, DIM=16, device=gpu, net=False)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+    st = torch.tensor([n, n * M], dtype=torch.int32, device=gpu)
+    _, _, cnt = pg.edges_loop(T(poses), T(pts), T(intr), T(ix), st, n - 1, M)
+    assert int(cnt.item()) == 0 and pg.errors == 4
+    pg.counts[2] = 0
+    _, _, cnt = pg.edges_loop(T(poses), T(pts), T(intr), T(ix), st, n, M)
+    assert int(cnt.item()) > 0 and pg.errors == 0
+
+
+def test_keyframe_delta_log_full_is_flagged(gpu):
+    """A frame drop whose pg.delta record finds the device log full keeps the
+    drop (as the reference) but sets patch-graph error bit 8 instead of
+    losing the record silently."""
+    from dpvo_amd.patchgraph import DevicePatchGraph
+
+    rng = np.random.default_rng(7)
+    N, M, P, n = 32, 10, 3, 20
+    step = np.where((np.arange(N) >= 14) & (np.arange(N) <= 18), 0.002, 0.05)
+    poses, pts, intr = _scene(rng, N, M, P, np.cumsum(step), n)
+    ii, jj, kk = _edges(n, M)
+    pg = DevicePatchGraph(max_edges=4096, DIM=16, device=gpu)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+    pg.append_factors(torch.arange(N * M, device=gpu) // M, T(kk), T(jj))
+    st = torch.tensor([n, n * M], dtype=torch.int32, device=gpu)
+    tstamps = T((np.arange(N) * 3 + 1).astype(np.int64))
+    log = (torch.zeros(1, 7, device=gpu), torch.zeros(1, 2, dtype=torch.long, device=gpu),
+           torch.ones(1, dtype=torch.int32, device=gpu))  # capacity 1, already holding 1
+    kf, _ = pg.keyframe(st, T(poses), T(pts), T(intr), M, tstamps=tstamps, delta=log)
+    assert kf.cpu().tolist()[0] == 1  # the drop happened
+    assert int(log[2].item()) == 1 and pg.errors == 8
+    assert st.cpu().tolist() == [n - 1, (n - 1) * M]
+
+
 def test_edges_loop_group_values_bit_exact(gpu):
     """the per-group flow magnitudes (the work buffer's first ng floats)
     equal the restatement's fp32 values bit for bit."""

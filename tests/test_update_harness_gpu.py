@@ -15,6 +15,7 @@ import pytest
 import torch
 
 import oracle
+from conftest import assert_ba_rel
 
 pytestmark = pytest.mark.gpu
 
@@ -93,6 +94,8 @@ def test_harness_frame_matches_oracle(gpu):
                        I["weight"].cpu().numpy(), 1e-4, I["ii"].cpu().numpy(), jj, kk, t0, t1,
                        h.ba_iters)
     P, K = h.poses.cpu().numpy(), h.patches.cpu().numpy()
+    # north_star's 1e-4 relative bar on the frame's pose / depth deltas
+    assert_ba_rel(P, K, Pr, Kr, I["poses"].cpu().numpy(), I["patches"].cpu().numpy(), t0, t1)
     np.testing.assert_allclose(P, Pr, rtol=0, atol=2e-5)
     np.testing.assert_allclose(K[:, 2], Kr[:, 2], rtol=1e-4, atol=1e-5)
     assert h.check() == 0
