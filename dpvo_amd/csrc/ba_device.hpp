@@ -22,7 +22,10 @@ __device__ __forceinline__ void tri_of(int bt, int& a, int& b) {  // bt -> (a, b
 // thread owns a contiguous run of at most kScanRun elements whose loads are
 // all issued before the first add (one LDS latency, not one per element).
 constexpr int kScanRun = 16;
-__device__ inline int fscan(int* data, int n, int* scr) {
+// pack_shift > 0: each input c is first replaced by (c << pack_shift) | (c > 0),
+// so one scan gives both the exclusive prefix of c (high bits) and the number
+// of nonzero entries before (low bits) -- bucket starts and bucket indices.
+__device__ inline int fscan(int* data, int n, int* scr, int pack_shift = 0) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const int per = (n + nt - 1) / nt;
   int total = 0;
@@ -33,6 +36,10 @@ __device__ inline int fscan(int* data, int n, int* scr) {
     int v[kScanRun];
 #pragma unroll
     for (int k = 0; k < kScanRun; k++) v[k] = (lo + k < hi) ? data[lo + k] : 0;
+    if (pack_shift > 0) {
+#pragma unroll
+      for (int k = 0; k < kScanRun; k++) v[k] = (v[k] << pack_shift) | (v[k] > 0 ? 1 : 0);
+    }
     int s = 0;
 #pragma unroll
     for (int k = 0; k < kScanRun; k++) s += v[k];

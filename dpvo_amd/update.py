@@ -37,7 +37,8 @@ drops t and n part, and the truth moves with the frame data.
 
 The update network (net.py) needs trained weights that are absent, so a
 deterministic "oracle network" stands in: delta = (true reprojection - coords)
-+ a fixed pseudo-random 0.1 px perturbation, weight = 0.5.  The frame features
++ a fixed pseudo-random perturbation of amplitude net_noise px (default 0.1),
+weight = 0.5.  The frame features
 are a fixed random field modulated per frame (deterministic, so an eager run
 and a graph replay produce the same bits).
 
@@ -62,12 +63,13 @@ class UpdateHarness:
     def __init__(self, device="cuda", M=20, lifetime=13, removal_window=22, opt_window=10,
                  mem=36, H=120, W=160, C=128, DIM=384, max_edges=10000, buffer=512,
                  ba_iters=1, seed=0, feat_dtype=torch.float32, pose_noise=0.01, depth_init=0.6,
-                 keyframes=False, keyframe_index=4, keyframe_thresh=12.5):
+                 keyframes=False, keyframe_index=4, keyframe_thresh=12.5, net_noise=0.1):
         self.dev = torch.device(device)
         self.M, self.r, self.rw, self.ow = M, lifetime, removal_window, opt_window
         self.mem = self.pmem = mem
         self.H, self.W, self.C = H, W, C
         self.ba_iters = ba_iters
+        self.net_noise = float(net_noise)
         self.keyframes, self.ki, self.kthresh = keyframes, keyframe_index, keyframe_thresh
         self.n = 0
         self.t = 0
@@ -179,7 +181,7 @@ class UpdateHarness:
         c = coords[..., self.P // 2, self.P // 2]
         h = (kk.float() * 12.9898 + jj.float() * 78.233 + 0.5 * self.fs[0:1].float())
         u = torch.stack([torch.sin(h), torch.cos(1.7 * h)], -1).view(c.shape)
-        delta = (true[..., self.P // 2, self.P // 2] - c) + 0.1 * u
+        delta = (true[..., self.P // 2, self.P // 2] - c) + self.net_noise * u
         weight = torch.full_like(c, 0.5)
         return delta, weight
 

@@ -42,7 +42,12 @@ for rep in range(40):
     if rep < 5:
         continue
     d = {"call (events)": e0.elapsed_time(e1) * 1e3, "kernel (marks)": (m[63] - m[0]) * 0.01,
-         "setup": (m[1] - m[0]) * 0.01}
+         "setup": (m[1] - m[0]) * 0.01,
+         "  setup: plan entries + counts": (m[40] - m[0]) * 0.01,
+         "  setup: scan": (m[41] - m[40]) * 0.01,
+         "  setup: records": (m[42] - m[41]) * 0.01,
+         "  setup: patch values, edge ids, poses": (m[43] - m[42]) * 0.01,
+         "  setup: per-edge inputs": (m[1] - m[43]) * 0.01}
     prev = 1
     for it in range(iters):
         mb = 2 + 8 * it

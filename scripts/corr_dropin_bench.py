@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    cc = altcorr.cuda_corr
+    from dpvo_amd.altcorr.correlation import cuda_corr as cc
     G = synthetic.make_config("cfg2", seed=0)
     D = G.to(dev)
     mem, R = 36, 3
