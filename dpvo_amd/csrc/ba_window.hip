@@ -162,25 +162,34 @@ __host__ __device__ constexpr size_t plan_lds_bytes(int cap) {
 }
 static_assert(plan_lds_bytes(kWMaxE) <= (size_t)kWLds, "plan LDS");
 
-__device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
-                                           const int64_t* __restrict__ jj,
-                                           const int64_t* __restrict__ kk, int E, int num_patches,
-                                           int num_poses, int t0, int N, const Plan& plan,
-                                           char* lds, int cap = kWMaxE) {
-  if (plan.t0d) t0 = *plan.t0d;
-  // LDS (plan_lds_bytes(cap), cap >= E; 153.9 KB at kWMaxE = 10240): per-edge
-  // arrays as u16 / u8, one union
-  //   [ctl 256 B | code u16[cap] | key u16[cap] -> ranked | spos u16[cap] | head u8[cap] | U]
-  //   U (>= 16 cap B): counting sort hist int[R], later hd int[E] + mask u32[E];
-  //      bitonic sort keys (u64 for E <= 8192, u32 (key << 14 | e) above)
+// rank of edge e among the members s[a, b) of its bucket (how many are smaller):
+// 8 LDS reads in flight per step instead of one dependent read per member
+__device__ __forceinline__ int bucket_rank(const unsigned short* s, int a, int b, int e) {
+  int rank = 0;
+  for (int t = a; t < b; t += 8) {
+    int v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = s[min(t + k, b - 1)];
+#pragma unroll
+    for (int k = 0; k < 8; k++) rank += (t + k < b && v[k] < e) ? 1 : 0;
+  }
+  return rank;
+}
+
+constexpr int kPlanPer = kWMaxE / kPT;  // edges per plan thread: e = tid + r * kPT
+// The plan's pass over the edge list: clamped kk of the thread's edges into
+// kv (registers), pose codes into code[e] (LDS), and the block-wide kmin / kmax
+// (ctl[0], ctl[1]), fmin (ctl[2], the smallest fixed pose) and status (ctl[3]).
+// Loads in rounds of kPlanRound edges per thread, every load of a round issued
+// before its first use (one global round trip per round); indices are clamped
+// instead of guarded (a guarded load is a branch with its own wait).  Ends
+// with a barrier.
+__device__ __forceinline__ void plan_edges_pass(const int64_t* __restrict__ ii,
+                                                const int64_t* __restrict__ jj,
+                                                const int64_t* __restrict__ kk, int E,
+                                                int num_patches, int num_poses, int t0, int N,
+                                                int* ctl, unsigned short* code, int (&kv)[kPlanPer]) {
   const int tid = threadIdx.x, lane = tid & 63, T = kPT;
-  int* ctl = (int*)lds;                  // [64]
-  int* scr = ctl + 16;                   // scan scratch [>= 17]
-  unsigned short* code = (unsigned short*)(lds + 256);           // ci | cj << 8 (5 bits each)
-  unsigned short* key = code + cap;                              // kk - kmin, later ranked edges
-  unsigned short* spos = key + cap;                              // edge at position p
-  unsigned char* head = (unsigned char*)(spos + cap);            // head flags
-  char* U = (char*)head + al16(cap);
   const int kmaxc = num_patches - 1;
   if (tid == 0) {
     ctl[0] = 0x7fffffff;  // kmin
@@ -189,41 +198,44 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
     ctl[3] = 0;           // status
   }
   __syncthreads();
-  constexpr int kPer = kWMaxE / kPT;  // edges per thread: e = tid + r * T
-  int kv[kPer];                      // clamped kk of this thread's edges (registers)
+  constexpr int kPlanRound = 5;
+  static_assert(kPlanPer % kPlanRound == 0, "load rounds");
   int kmin = 0x7fffffff, kmax = -1, fmin = 0x7fffffff, bad = 0;
-  // the edge list in rounds of 8 edges per thread, every load of a round issued
-  // before its first use (one global round trip per round)
+  if (E > 0) {
 #pragma unroll
-  for (int r0 = 0; r0 < kPer; r0 += 4) {
-    int64_t vk[4], vi[4], vj[4];
+    for (int r0 = 0; r0 < kPlanPer; r0 += kPlanRound) {
+      int64_t vk[kPlanRound], vi[kPlanRound], vj[kPlanRound];
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int e = tid + (r0 + r) * T;
-      vk[r] = (e < E) ? kk[e] : 0;
-      vi[r] = (e < E) ? ii[e] : 0;
-      vj[r] = (e < E) ? jj[e] : 0;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int e = tid + (r0 + r) * T;
-      kv[r0 + r] = 0;
-      if (e >= E) continue;
-      int64_t v = vk[r];
-      if (v < 0 || v > kmaxc) {
-        bad = 1;
-        v = v < 0 ? 0 : kmaxc;
+      for (int r = 0; r < kPlanRound; r++) {
+        const int e = min(tid + (r0 + r) * T, E - 1);
+        vk[r] = kk[e];
+        vi[r] = ii[e];
+        vj[r] = jj[e];
       }
-      kmin = min(kmin, (int)v);
-      kmax = max(kmax, (int)v);
-      kv[r0 + r] = (int)v;
-      const int64_t gi = vi[r], gj = vj[r];
-      const bool fi = gi >= t0 && gi < t0 + N, fj = gj >= t0 && gj < t0 + N;
-      const int ci = fi ? (int)(gi - t0) : (int)kFix, cj = fj ? (int)(gj - t0) : (int)kFix;
-      if (!fi) fmin = min(fmin, (int)min(max(gi, (int64_t)0), (int64_t)num_poses - 1));
-      if (!fj) fmin = min(fmin, (int)min(max(gj, (int64_t)0), (int64_t)num_poses - 1));
-      code[e] = (unsigned short)((ci & 0xff) | ((cj & 0xff) << 8));
+#pragma unroll
+      for (int r = 0; r < kPlanRound; r++) {
+        const int e = tid + (r0 + r) * T;
+        kv[r0 + r] = 0;
+        if (e >= E) continue;
+        int64_t v = vk[r];
+        if (v < 0 || v > kmaxc) {
+          bad = 1;
+          v = v < 0 ? 0 : kmaxc;
+        }
+        kmin = min(kmin, (int)v);
+        kmax = max(kmax, (int)v);
+        kv[r0 + r] = (int)v;
+        const int64_t gi = vi[r], gj = vj[r];
+        const bool fi = gi >= t0 && gi < t0 + N, fj = gj >= t0 && gj < t0 + N;
+        const int ci = fi ? (int)(gi - t0) : (int)kFix, cj = fj ? (int)(gj - t0) : (int)kFix;
+        if (!fi) fmin = min(fmin, (int)min(max(gi, (int64_t)0), (int64_t)num_poses - 1));
+        if (!fj) fmin = min(fmin, (int)min(max(gj, (int64_t)0), (int64_t)num_poses - 1));
+        code[e] = (unsigned short)((ci & 0xff) | ((cj & 0xff) << 8));
+      }
     }
+  } else {
+#pragma unroll
+    for (int r = 0; r < kPlanPer; r++) kv[r] = 0;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -239,7 +251,31 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
     if (bad) atomicOr(&ctl[3], kStClamp);
   }
   __syncthreads();
-  kmin = ctl[0];
+}
+
+__device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
+                                           const int64_t* __restrict__ jj,
+                                           const int64_t* __restrict__ kk, int E, int num_patches,
+                                           int num_poses, int t0, int N, const Plan& plan,
+                                           char* lds, int cap = kWMaxE) {
+  if (plan.t0d) t0 = *plan.t0d;
+  // LDS (plan_lds_bytes(cap), cap >= E; 153.9 KB at kWMaxE = 10240): per-edge
+  // arrays as u16 / u8, one union
+  //   [ctl 256 B | code u16[cap] | key u16[cap] -> ranked | spos u16[cap] | head u8[cap] | U]
+  //   U (>= 16 cap B): counting sort hist int[R], later hd int[E] + mask u32[E];
+  //      bitonic sort keys (u64 for E <= 8192, u32 (key << 14 | e) above)
+  const int tid = threadIdx.x, T = kPT;
+  const int kmaxc = num_patches - 1;
+  int* ctl = (int*)lds;                  // [64]
+  int* scr = ctl + 16;                   // scan scratch [>= 17]
+  unsigned short* code = (unsigned short*)(lds + 256);           // ci | cj << 8 (5 bits each)
+  unsigned short* key = code + cap;                              // kk - kmin, later ranked edges
+  unsigned short* spos = key + cap;                              // edge at position p
+  unsigned char* head = (unsigned char*)(spos + cap);            // head flags
+  char* U = (char*)head + al16(cap);
+  int kv[kPlanPer];  // clamped kk of this thread's edges e = tid + r * kPT (registers)
+  plan_edges_pass(ii, jj, kk, E, num_patches, num_poses, t0, N, ctl, code, kv);
+  int kmin = ctl[0];
   const int R = ctl[1] - kmin + 1;
   if (R <= kHistMax && (size_t)(R + E) * 4 <= plan_u_bytes(cap) && E < (1 << 14)) {
     // ---- counting sort in ONE scan (no second pass over positions) ----
@@ -255,14 +291,14 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
     for (int u = tid; u < E; u += T) pm[u] = 0u;
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kPer; r++) {
+    for (int r = 0; r < kPlanPer; r++) {
       const int e = tid + r * T;
       if (e < E) atomicAdd(&hist[kv[r] - kmin], 1);
     }
     __syncthreads();
     const int nuniq = fscan(hist, R, scr, 14) & 0x3fff;  // hist[v] = start << 14 | patch
 #pragma unroll
-    for (int r = 0; r < kPer; r++) {
+    for (int r = 0; r < kPlanPer; r++) {
       const int e = tid + r * T;
       if (e >= E) continue;
       const int old = atomicAdd(&hist[kv[r] - kmin], 1 << 14);
@@ -275,13 +311,12 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
     // hist[v] >> 14 is now the END of bucket v (= the start of bucket v + 1);
     // the patch index bits are unchanged
 #pragma unroll
-    for (int r = 0; r < kPer; r++) {
+    for (int r = 0; r < kPlanPer; r++) {
       const int e = tid + r * T;
       if (e >= E) continue;
       const int v = kv[r] - kmin, hv = hist[v];
       const int b = hv >> 14, a = (v == 0) ? 0 : (hist[v - 1] >> 14);
-      int rank = 0;
-      for (int t = a; t < b; t++) rank += ((int)spos[t] < e) ? 1 : 0;
+      const int rank = bucket_rank(spos, a, b, e);
       plan.epos[a + rank] = e;
       if (rank == 0) {
         const int u = hv & 0x3fff;
@@ -307,7 +342,7 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
     for (int p = tid; p < E; p += T) head[p] = 0;
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kPer; r++) {
+    for (int r = 0; r < kPlanPer; r++) {
       const int e = tid + r * T;
       if (e < E) atomicAdd(&hist[kv[r] - kmin], 1);
     }
@@ -322,7 +357,7 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
     // middle of a bucket: patches split or merged, a wrong Schur complement)
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kPer; r++) {
+    for (int r = 0; r < kPlanPer; r++) {
       const int e = tid + r * T;
       if (e < E) spos[atomicAdd(&hist[kv[r] - kmin], 1)] = (unsigned short)e;
     }
@@ -330,21 +365,19 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
     // deterministic order inside a patch (ascending edge index): every edge
     // counts the smaller edges of its bucket, all edges in parallel; the
     // ranked order overwrites the keys (no longer read) after a barrier
-    int dst[kPer];
+    int dst[kPlanPer];
 #pragma unroll
-    for (int r = 0; r < kPer; r++) {
+    for (int r = 0; r < kPlanPer; r++) {
       const int e = tid + r * T;
       dst[r] = -1;
       if (e >= E) continue;
       const int v = kv[r] - kmin;
       const int b = hist[v], a = (v == 0) ? 0 : hist[v - 1];  // hist[v]: end of bucket v now
-      int rank = 0;
-      for (int t = a; t < b; t++) rank += ((int)spos[t] < e) ? 1 : 0;
-      dst[r] = a + rank;
+      dst[r] = a + bucket_rank(spos, a, b, e);
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kPer; r++)
+    for (int r = 0; r < kPlanPer; r++)
       if (dst[r] >= 0) key[dst[r]] = (unsigned short)(tid + r * T);
     pos_edge = key;
   } else {
@@ -360,7 +393,7 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
     unsigned long long* k64 = (unsigned long long*)U;
     unsigned* k32 = (unsigned*)U;
 #pragma unroll
-    for (int r = 0; r < kPer; r++) {
+    for (int r = 0; r < kPlanPer; r++) {
       const int e = tid + r * T;
       if (e < E) {
         if (wide)
@@ -449,13 +482,145 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
   }
 }
 
+// ---- the plan over S workgroups (shard s of S) ----
+// Every shard makes the pass over the whole edge list (kk / ii / jj of 10k
+// edges = 240 KB, L2-resident after the first shard), so kmin / kmax / fmin /
+// status and the presence bitmap of patch ids are known everywhere; shard s
+// then groups only the edges of ITS bucket range [lo, hi) of kk - kmin:
+//   positions  = edges with a smaller kk (counted in the pass) + the local
+//                counting sort,
+//   patch ids  = present kk values below lo (bitmap popcount) + local index.
+// The shards write disjoint ranges of epos / poff / pkk / pmask: no exchange
+// between workgroups.  Falls back to plan_block in shard 0 when the kk range
+// or the LDS does not fit.
+constexpr int kPlanShardMax = 16;
+__host__ __device__ constexpr int plan_shards(int E) {
+  return E <= 512 ? 1 : ((E + 511) / 512 < kPlanShardMax ? (E + 511) / 512 : kPlanShardMax);
+}
+__device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
+                                             const int64_t* __restrict__ jj,
+                                             const int64_t* __restrict__ kk, int E, int num_patches,
+                                             int num_poses, int t0, int N, const Plan& plan,
+                                             char* lds, int cap, size_t lds_bytes, int s, int S) {
+  if (S <= 1) {
+    if (s == 0) plan_block(ii, jj, kk, E, num_patches, num_poses, t0, N, plan, lds, cap);
+    return;
+  }
+  if (plan.t0d) t0 = *plan.t0d;
+  //   [ctl 256 B | code u16[cap] | spos u16[cap] | pres u32[kHistMax / 32] | hist int[nl] | pm u32[nl]]
+  const int tid = threadIdx.x, lane = tid & 63, T = kPT;
+  int* ctl = (int*)lds;  // [0..3] as plan_edges_pass, [4] below, [5] ubelow, [6] nuniq
+  int* scr = ctl + 16;
+  unsigned short* code = (unsigned short*)(lds + 256);
+  unsigned short* spos = code + cap;
+  unsigned* pres = reinterpret_cast<unsigned*>(spos + cap);
+  int* hist = reinterpret_cast<int*>(pres + kHistMax / 32);
+  int kv[kPlanPer];
+  plan_edges_pass(ii, jj, kk, E, num_patches, num_poses, t0, N, ctl, code, kv);
+  const int kmin = ctl[0], R = ctl[1] - kmin + 1;
+  const int nlmax = (R + S - 1) / S;
+  const bool fits = E > 0 && R <= kHistMax && E < (1 << 14) &&
+                    256 + 4 * (size_t)cap + 4 * (size_t)(kHistMax / 32) + 8 * (size_t)nlmax <= lds_bytes;
+  if (!fits) {  // shard-uniform (every shard saw the same edges)
+    if (s == 0) {
+      __syncthreads();  // ctl is re-initialised by plan_block
+      plan_block(ii, jj, kk, E, num_patches, num_poses, t0, N, plan, lds, cap);
+    }
+    return;
+  }
+  const int lo = (int)((long long)R * s / S), hi = (int)((long long)R * (s + 1) / S), nl = hi - lo;
+  unsigned* pm = reinterpret_cast<unsigned*>(hist + nl);
+  const int nw = (R + 31) >> 5;
+  for (int w = tid; w < nw; w += T) pres[w] = 0u;
+  for (int v = tid; v < nl; v += T) {
+    hist[v] = 0;
+    pm[v] = 0u;
+  }
+  if (tid == 0) {
+    ctl[4] = 0;
+    ctl[5] = 0;
+    ctl[6] = 0;
+  }
+  __syncthreads();
+  int nb = 0;
+#pragma unroll
+  for (int r = 0; r < kPlanPer; r++) {
+    const int e = tid + r * T;
+    if (e >= E) continue;
+    const int v = kv[r] - kmin;
+    atomicOr(&pres[v >> 5], 1u << (v & 31));
+    if (v < lo) nb++;
+    else if (v < hi) atomicAdd(&hist[v - lo], 1);
+  }
+  __syncthreads();  // presence bitmap complete
+  int ub = 0, nu = 0;
+  for (int w = tid; w < nw; w += T) {
+    const unsigned x = pres[w];
+    const int b0 = 32 * w;
+    nu += __popc(x);
+    ub += (b0 + 32 <= lo) ? __popc(x) : (b0 < lo ? __popc(x & ((1u << (lo - b0)) - 1u)) : 0);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    nb += __shfl_xor(nb, o, 64);
+    ub += __shfl_xor(ub, o, 64);
+    nu += __shfl_xor(nu, o, 64);
+  }
+  if (lane == 0) {
+    atomicAdd(&ctl[4], nb);
+    atomicAdd(&ctl[5], ub);
+    atomicAdd(&ctl[6], nu);
+  }
+  // local counting sort in one packed scan (plan_block's fast path); the
+  // scan's barriers also complete the ctl sums above
+  fscan(hist, nl, scr, 14);
+  const int below = ctl[4], ubelow = ctl[5], nuniq = ctl[6];
+#pragma unroll
+  for (int r = 0; r < kPlanPer; r++) {
+    const int e = tid + r * T;
+    const int v = kv[r] - kmin - lo;
+    if (e >= E || v < 0 || v >= nl) continue;
+    const int old = atomicAdd(&hist[v], 1 << 14);
+    spos[old >> 14] = (unsigned short)e;
+    const unsigned c = code[e], ci = c & 0xff, cj = c >> 8;
+    const unsigned m = (ci != kFix ? 1u << ci : 0u) | (cj != kFix ? 1u << cj : 0u);
+    if (m) atomicOr(&pm[old & 0x3fff], m);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kPlanPer; r++) {
+    const int e = tid + r * T;
+    const int v = kv[r] - kmin - lo;
+    if (e >= E || v < 0 || v >= nl) continue;
+    const int hv = hist[v];
+    const int b = hv >> 14, a = (v == 0) ? 0 : (hist[v - 1] >> 14);
+    const int rank = bucket_rank(spos, a, b, e);
+    plan.epos[below + a + rank] = e;
+    if (rank == 0) {
+      const int u = ubelow + (hv & 0x3fff);
+      plan.poff[u] = below + a;
+      plan.pkk[u] = kv[r];
+      plan.pmask[u] = pm[hv & 0x3fff];
+    }
+  }
+  if (tid == 0 && s == S - 1) plan.poff[nuniq] = E;
+  if (tid == 0 && s == 0) {
+    plan.meta[0] = nuniq;
+    plan.meta[1] = ctl[2];
+    plan.meta[2] = ctl[3];
+    if (ctl[3] && plan.sink) atomicOr(plan.sink, ctl[3]);
+    *plan.status = 0;
+  }
+}
+
 __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict__ ii,
                                                       const int64_t* __restrict__ jj,
                                                       const int64_t* __restrict__ kk, int E,
                                                       int num_patches, int num_poses, int t0, int N,
                                                       Plan plan) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  plan_block(ii, jj, kk, E, num_patches, num_poses, t0, N, plan, lds);
+  plan_sharded(ii, jj, kk, E, num_patches, num_poses, t0, N, plan, lds, kWMaxE, kWLds, blockIdx.x,
+               gridDim.x);
 }
 
 // One launch for the start of a DPVO update (dpvo.py:775-824): F-REPROJ of
@@ -473,20 +638,22 @@ struct RArgs {
   int E, P, num_poses, num_patches, N2, t0, N;
   float* coords;
   int* order;
+  int nps;  // plan shards: workgroups [0, nps) plan, nps the edge order, then the reprojection
 };
 
 __global__ void __launch_bounds__(kPT) reproject_plan_kernel(RArgs R, Plan plan) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  if (blockIdx.x == 0) {
-    plan_block(R.ii, R.jj, R.kk, R.E, R.num_patches, R.num_poses, R.t0, R.N, plan, lds);
+  if ((int)blockIdx.x < R.nps) {
+    plan_sharded(R.ii, R.jj, R.kk, R.E, R.num_patches, R.num_poses, R.t0, R.N, plan, lds, kWMaxE,
+                 kWLds, blockIdx.x, R.nps);
     return;
   }
-  if (blockIdx.x == 1) {
+  if ((int)blockIdx.x == R.nps) {
     edge_order_block(R.jj, R.E, R.N2, R.order, reinterpret_cast<int*>(lds));
     return;
   }
   const int PP = R.P * R.P;
-  const int t = (blockIdx.x - 2) * kPT + threadIdx.x;
+  const int t = (blockIdx.x - R.nps - 1) * kPT + threadIdx.x;
   if (t >= R.E * PP) return;
   reproject_pixel(R.poses, R.patches, R.intrinsics, R.ii, R.jj, R.kk, t / PP, t % PP, R.P,
                   R.num_poses, R.num_patches, R.coords);
@@ -508,26 +675,26 @@ template <typename T>
 __global__ void __launch_bounds__(kPT) reproject_plan_insert_kernel(RArgs R, Plan plan, InsArgs I,
                                                                     int nrep) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int b = blockIdx.x;
-  if (b == 0) {
-    plan_block(R.ii, R.jj, R.kk, R.E, R.num_patches, R.num_poses, R.t0, R.N, plan, lds,
-               plan_cap(R.E));
+  const int b = blockIdx.x, b0 = R.nps + 1;  // first reprojection workgroup
+  if (b < R.nps) {
+    plan_sharded(R.ii, R.jj, R.kk, R.E, R.num_patches, R.num_poses, R.t0, R.N, plan, lds,
+                 plan_cap(R.E), plan_lds_bytes(plan_cap(R.E)), b, R.nps);
     return;
   }
-  if (b == 1) {
+  if (b == R.nps) {
     edge_order_block(R.jj, R.E, R.N2, R.order, reinterpret_cast<int*>(lds));
     return;
   }
-  if (b < 2 + nrep) {
+  if (b < b0 + nrep) {
     const int PP = R.P * R.P;
-    const int t = (b - 2) * kPT + threadIdx.x;
+    const int t = (b - b0) * kPT + threadIdx.x;
     if (t >= R.E * PP) return;
     reproject_pixel(R.poses, R.patches, R.intrinsics, R.ii, R.jj, R.kk, t / PP, t % PP, R.P,
                     R.num_poses, R.num_patches, R.coords);
     return;
   }
   static_assert(kPT == 512, "two 256-thread insertion tiles per workgroup");
-  const int half = threadIdx.x >> 8, t = 2 * (b - 2 - nrep) + half;
+  const int half = threadIdx.x >> 8, t = 2 * (b - b0 - nrep) + half;
   const bool act = t < I.ntile;
   const int tt = act ? t : 0;
   float* tile = reinterpret_cast<float*>(lds) + half * kInsTC * kInsCS;
@@ -2308,7 +2475,7 @@ int ba_window_plan(const int64_t* ii, const int64_t* jj, const int64_t* kk, int 
   set_attrs();
   Plan plan = plan_view(scratch, E, status);
   plan.t0d = t0d;
-  hipLaunchKernelGGL(ba_plan_kernel, dim3(1), dim3(kPT), kWLds, as_stream(stream), ii, jj, kk, E,
+  hipLaunchKernelGGL(ba_plan_kernel, dim3(plan_shards(E)), dim3(kPT), kWLds, as_stream(stream), ii, jj, kk, E,
                      num_patches, num_poses, t0, t1 - t0, plan);
   return launch_status();
 }
@@ -2339,8 +2506,9 @@ int ba_window_reproject_plan(const float* poses, const float* patches, const flo
   r.N = t1 - t0;
   r.coords = coords;
   r.order = order;
+  r.nps = plan_shards(E);
   const int total = E * P * P;
-  hipLaunchKernelGGL(reproject_plan_kernel, dim3(2 + (total + kPT - 1) / kPT), dim3(kPT), kWLds,
+  hipLaunchKernelGGL(reproject_plan_kernel, dim3(r.nps + 1 + (total + kPT - 1) / kPT), dim3(kPT), kWLds,
                      as_stream(stream), r, plan);
   return launch_status();
 }
@@ -2373,6 +2541,7 @@ int ba_window_reproject_plan_insert(const float* poses, const float* patches,
   r.N = t1 - t0;
   r.coords = coords;
   r.order = order;
+  r.nps = plan_shards(E);
   InsArgs I = {};
   I.src = src;
   I.L = L;
@@ -2388,7 +2557,7 @@ int ba_window_reproject_plan_insert(const float* poses, const float* patches,
   I.gy = (H + kInsTY - 1) / kInsTY;
   I.ntile = I.gx * I.gy * ((C + kInsTC - 1) / kInsTC);
   const int nrep = (E * P * P + kPT - 1) / kPT;
-  const dim3 grid(2 + nrep + (I.ntile + 1) / 2);
+  const dim3 grid(r.nps + 1 + nrep + (I.ntile + 1) / 2);
   // LDS sized for this E (the plan's need), not the kWMaxE maximum: the
   // insertion tiles then run several workgroups per CU beside the plan
   size_t lds = plan_lds_bytes(plan_cap(E));

@@ -264,9 +264,10 @@ def _plan_arrays(cb, ws, E, t0, t1):
     def arr(k, n, dt):
         return np.frombuffer(b[off[k]:off[k] + 4 * n].tobytes(), dt)
 
-    nuniq = int(arr(4, 8, np.int32)[0])
+    meta = arr(4, 8, np.int32)
+    nuniq = int(meta[0])
     return (arr(0, E, np.int32), arr(1, nuniq + 1, np.int32), arr(2, nuniq, np.uint32),
-            arr(3, nuniq, np.int32), nuniq)
+            arr(3, nuniq, np.int32), nuniq, meta)
 
 
 @pytest.mark.parametrize("E,nk,M,seed", [(96, 40, 1024, 0), (700, 650, 1024, 1),
@@ -278,7 +279,9 @@ def test_plan_grouping_matches_host(cb, gpu, E, nk, M, seed):
     """Regression for the plan's counting sort (the head flags of every
     bucket are read before any wave bumps a bucket counter): many small
     buckets and E > 64, through fastba.plan and the fused reprojection launch,
-    the grouping is exactly the host one, on repeated calls.  M = 2048 / 4096
+    the grouping is exactly the host one, on repeated calls; E > 512 runs the
+    sharded plan (one workgroup per kk range) when the kk range fits the
+    counting sort.  M = 2048 / 4096
     put the kk range past the counting sort's (bitonic path: 64-bit keys up
     to E = 8192, packed 32-bit keys above)."""
     from dpvo_amd import fastba
@@ -292,12 +295,16 @@ def test_plan_grouping_matches_host(cb, gpu, E, nk, M, seed):
     ii = kk // M
     jj = rng.integers(0, F, E).astype(np.int64)
     ref = _host_grouping(ii, jj, kk, t0, t1)
+    both = np.concatenate([ii, jj])
+    fixed = both[(both < t0) | (both >= t1)]
+    fmin = int(np.clip(fixed.min(), 0, F - 1)) if fixed.size else 2 ** 31 - 1
     D = [torch.from_numpy(x).to(gpu) for x in (ii, jj, kk)]
     for rep in range(3):
         ws = fastba.plan(*D, t0, t1, F * M, F)
         assert ws is not None
-        epos, poff, pmask, pkk, nuniq = _plan_arrays(cb, ws, E, t0, t1)
+        epos, poff, pmask, pkk, nuniq, meta = _plan_arrays(cb, ws, E, t0, t1)
         assert nuniq == ref[3].size
+        assert int(meta[1]) == fmin and int(meta[2]) == 0  # smallest fixed pose, no clamp
         np.testing.assert_array_equal(pkk, ref[3])
         np.testing.assert_array_equal(poff, ref[1])
         np.testing.assert_array_equal(epos, ref[0])
@@ -308,7 +315,9 @@ def test_plan_grouping_matches_host(cb, gpu, E, nk, M, seed):
     patches = torch.ones(F * M, 3, 3, 3, device=gpu)
     intr = torch.tensor([[80.0, 80.0, 80.0, 60.0]], device=gpu).repeat(F, 1)
     _, _, ws = fastba.reproject(poses, patches, intr, *D, mem=F, plan_window=(t0, t1))
-    epos, poff, pmask, pkk, _ = _plan_arrays(cb, ws, E, t0, t1)
+    epos, poff, pmask, pkk, nuniq, meta = _plan_arrays(cb, ws, E, t0, t1)
+    assert nuniq == ref[3].size and int(meta[1]) == fmin
+    np.testing.assert_array_equal(poff, ref[1])
     np.testing.assert_array_equal(epos, ref[0])
     np.testing.assert_array_equal(pkk, ref[3])
     np.testing.assert_array_equal(pmask, ref[2])
