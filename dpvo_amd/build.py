@@ -37,7 +37,7 @@ EXTENSIONS = {
     "cuda_ba": "ext_cuda_ba.cpp",
     "lietorch_backends": "ext_lietorch.cpp",
 }
-HEADERS = ["common.hpp", "ext_common.hpp", "ba_device.hpp", "ba_solve.hpp", "pyr_insert.hpp"]
+HEADERS = ["common.hpp", "ext_common.hpp", "ba_device.hpp", "ba_solve.hpp", "pyr_insert.hpp", "ba_bgj.hpp"]
 # per-source device flags.  The BA window kernel is a chain of short dependent
 # steps run by few waves: clang's SLP vectoriser packs its scalar fp32 math into
 # v_pk_fma_f32 and pays for it with register-pair v_mov shuffles (3x the

@@ -181,9 +181,9 @@ constexpr int kPlanPer = kWMaxE / kPT;  // edges per plan thread: e = tid + r * 
 // kv (registers), pose codes into code[e] (LDS), and the block-wide kmin / kmax
 // (ctl[0], ctl[1]), fmin (ctl[2], the smallest fixed pose) and status (ctl[3]).
 // Loads in rounds of kPlanRound edges per thread, every load of a round issued
-// before its first use (one global round trip per round); indices are clamped
-// instead of guarded (a guarded load is a branch with its own wait).  Ends
-// with a barrier.
+// before its first use (one global round trip per round, and only the rounds
+// that hold edges); indices are clamped instead of guarded (a guarded load is
+// a branch with its own wait).  Ends with a barrier.
 __device__ __forceinline__ void plan_edges_pass(const int64_t* __restrict__ ii,
                                                 const int64_t* __restrict__ jj,
                                                 const int64_t* __restrict__ kk, int E,
@@ -201,9 +201,12 @@ __device__ __forceinline__ void plan_edges_pass(const int64_t* __restrict__ ii,
   constexpr int kPlanRound = 5;
   static_assert(kPlanPer % kPlanRound == 0, "load rounds");
   int kmin = 0x7fffffff, kmax = -1, fmin = 0x7fffffff, bad = 0;
+#pragma unroll
+  for (int r = 0; r < kPlanPer; r++) kv[r] = 0;
   if (E > 0) {
 #pragma unroll
     for (int r0 = 0; r0 < kPlanPer; r0 += kPlanRound) {
+      if (r0 * T >= E) break;  // block-uniform: only the rounds that hold edges (one at cfg2)
       int64_t vk[kPlanRound], vi[kPlanRound], vj[kPlanRound];
 #pragma unroll
       for (int r = 0; r < kPlanRound; r++) {
@@ -215,7 +218,6 @@ __device__ __forceinline__ void plan_edges_pass(const int64_t* __restrict__ ii,
 #pragma unroll
       for (int r = 0; r < kPlanRound; r++) {
         const int e = tid + (r0 + r) * T;
-        kv[r0 + r] = 0;
         if (e >= E) continue;
         int64_t v = vk[r];
         if (v < 0 || v > kmaxc) {
@@ -233,9 +235,6 @@ __device__ __forceinline__ void plan_edges_pass(const int64_t* __restrict__ ii,
         code[e] = (unsigned short)((ci & 0xff) | ((cj & 0xff) << 8));
       }
     }
-  } else {
-#pragma unroll
-    for (int r = 0; r < kPlanPer; r++) kv[r] = 0;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1726,6 +1725,7 @@ __global__ void __launch_bounds__(kWT) ba_dense_kernel(WArgs A) {
       __hip_atomic_load(&A.flags[kEpochWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
   const int nuniq = A.plan.meta[0], fmin = A.plan.meta[1];
   mark(A, 0);
+  if (A.marks && g == 0 && tid == 0) A.marks[59] = 0;
   WL L;  // shared header: ctl, pose table, dX, block table
   L.ctl = (int*)lds;
   int* ctl = L.ctl;
@@ -1920,6 +1920,7 @@ __global__ void __launch_bounds__(kWT) ba_dense_kernel(WArgs A) {
       const int e1 = min(e1r, e0 + kDChunk);
       for (int t = tid; t < kDMw * NB; t += kWT) D.bm[t] = 0u;
       __syncthreads();
+      if (it == 0 && pa == 0) mark(A, 55);
       // (1) thread per edge: the reference's fp32 linearisation; the edge joins
       // the masks of the (at most 3) blocks it adds to
       for (int q = e0 + tid; q < e1; q += kWT) {
@@ -1949,6 +1950,7 @@ __global__ void __launch_bounds__(kWT) ba_dense_kernel(WArgs A) {
         }
       }
       __syncthreads();
+      if (it == 0 && pa == 0) mark(A, 56);  // diagnostics: pass 0 sub-stages of workgroup 0
       // (2) thread per (own patch, slot): C, u (slot 0) and the E column block at
       // the slot's pose, edges in order (fp64 products of the fp32 terms)
       {
@@ -1970,17 +1972,23 @@ __global__ void __launch_bounds__(kWT) ba_dense_kernel(WArgs A) {
             const unsigned c = D.ec[q];
             const unsigned ci = (c & 0xff) < (unsigned)N ? (c & 0xff) : kFix;
             const unsigned cj = (c >> 8) < (unsigned)N ? (c >> 8) : kFix;
+            // every value read unconditionally, then selected: a load under
+            // the select compiles to a branch that waits for it alone
+            float jr[30];
+#pragma unroll
+            for (int t = 0; t < 30; t++) jr[t] = j[t];
 #pragma unroll
             for (int row = 0; row < 2; row++) {
-              const double wr = j[row], wz = wr * (double)j[4 + row];
-              if (k == 0) {
-                C += wz * (double)j[4 + row];
-                U += (wr * (double)j[2 + row]) * (double)j[4 + row];
-              }
+              const double wr = jr[row], wz = wr * (double)jr[4 + row];
+              const double cC = wz * (double)jr[4 + row];
+              const double cU = (wr * (double)jr[2 + row]) * (double)jr[4 + row];
+              C += (k == 0) ? cC : 0.0;
+              U += (k == 0) ? cU : 0.0;
 #pragma unroll
               for (int x = 0; x < 6; x++) {
-                Ev[x] += (cj == p) ? wz * (double)j[18 + 6 * row + x] : 0.0;
-                Ev[x] -= (ci == p) ? wz * (double)j[6 + 6 * row + x] : 0.0;
+                const double pj = wz * (double)jr[18 + 6 * row + x], pi = wz * (double)jr[6 + 6 * row + x];
+                Ev[x] += (cj == p) ? pj : 0.0;
+                Ev[x] -= (ci == p) ? pi : 0.0;
               }
             }
           }
@@ -1991,6 +1999,7 @@ __global__ void __launch_bounds__(kWT) ba_dense_kernel(WArgs A) {
         }
       }
       __syncthreads();
+      if (it == 0 && pa == 0) mark(A, 57);
       // (3) thread per (block, row) item: B terms of the pass's edges (ba_cuda.cu:
       // 339-370), then the Schur terms of its patches (:554-558), fixed order
 #pragma unroll
@@ -2009,21 +2018,25 @@ __global__ void __launch_bounds__(kWT) ba_dense_kernel(WArgs A) {
           const bool ia = ci == ua, ja = cj == ua, ib = ci == ub, jb = cj == ub;
           if (!(dg ? (ia || ja) : ((ia && jb) || (ja && ib)))) continue;
           const float* j = D.J + kDJs * (q - e0);
+          float jr[30];  // unconditional reads, selects below (see stage 2)
+#pragma unroll
+          for (int t = 0; t < 30; t++) jr[t] = j[t];
 #pragma unroll
           for (int row = 0; row < 2; row++) {
-            const double wr = j[row];
+            const double wr = jr[row];
             double Rv, Cv[6];
+            const double xi = jr[6 + 6 * row + x], xj = jr[18 + 6 * row + x];
             if (dg) {
-              Rv = (ia ? (double)j[6 + 6 * row + x] : 0.0) - (ja ? (double)j[18 + 6 * row + x] : 0.0);
+              Rv = (ia ? xi : 0.0) - (ja ? xj : 0.0);
 #pragma unroll
               for (int z = 0; z < 6; z++)
-                Cv[z] = (ia ? (double)j[6 + 6 * row + z] : 0.0) - (ja ? (double)j[18 + 6 * row + z] : 0.0);
-              acc[k][6] -= (wr * (double)j[2 + row]) * Rv;
+                Cv[z] = (ia ? (double)jr[6 + 6 * row + z] : 0.0) - (ja ? (double)jr[18 + 6 * row + z] : 0.0);
+              acc[k][6] -= (wr * (double)jr[2 + row]) * Rv;
             } else {
-              Rv = ia ? (double)j[6 + 6 * row + x] : (double)j[18 + 6 * row + x];
+              Rv = ia ? xi : xj;
 #pragma unroll
               for (int z = 0; z < 6; z++)
-                Cv[z] = ia ? (double)j[18 + 6 * row + z] : (double)j[6 + 6 * row + z];
+                Cv[z] = ia ? (double)jr[18 + 6 * row + z] : (double)jr[6 + 6 * row + z];
             }
             const double t = (dg ? wr : -wr) * Rv;
 #pragma unroll
@@ -2044,7 +2057,13 @@ __global__ void __launch_bounds__(kWT) ba_dense_kernel(WArgs A) {
         }
       }
       __syncthreads();
+      if (it == 0 && pa == 0) mark(A, 58);
+      if (it == 0 && A.marks && g == 0 && tid == 0) A.marks[59]++;  // passes
       pa = pb;
+    }
+    if (it == 0 && A.marks && g == 0 && tid == 0) {
+      A.marks[60] = D.ne;
+      A.marks[61] = D.np;
     }
     mark(A, mb + 4);
     if (A.marks && tid == 0 && it == 0 && g < 256) A.marks[1408 + g] = (int64_t)wall_clock64();

@@ -187,11 +187,10 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     }
   }
   auto build_A = [&]() __attribute__((always_inline)) {
+    // unconditional: lanes past the end rewrite the last unit with its own value
 #pragma unroll
-    for (int r = 0; r < kRA; r++) {
-      const int v = lane + kWave * r;
-      if (v < n16) reinterpret_cast<u32x4*>(G)[v] = st[r];
-    }
+    for (int r = 0; r < kRA; r++)
+      reinterpret_cast<u32x4*>(G)[min(lane + kWave * r, n16 - 1)] = st[r];
     wave_lds_sync();
     const bool arow = idx_ok && ai < np;
     if constexpr (kHalf) {
@@ -407,9 +406,12 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     pnpx[j] = bw0 * wave_uniform(gg->bh);
     prbw[j] = 1.0f / (float)bw0;
     prow[j] = W2 * C;
+    // an empty box reads the frame's first pixel (in range whatever the
+    // coordinates): the ring preload below is then unconditional
+    const bool empty = wave_uniform(gg->bw) <= 0 || wave_uniform(gg->bh) <= 0;
     pbase[j] = static_cast<const T*>(LV_SEL(f2, l)) +
                (((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 +
-                (size_t)wave_uniform(gg->ylo) * W2 + wave_uniform(gg->xlo)) * C;
+                (empty ? 0 : (size_t)wave_uniform(gg->ylo) * W2 + wave_uniform(gg->xlo))) * C;
   }
   auto pick = [](int j, auto a0, auto a1, auto a2, auto a3) __attribute__((always_inline)) {
     return j == 0 ? a0 : j == 1 ? a1 : j == 2 ? a2 : a3;
@@ -445,19 +447,19 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     }
   };
   u32x4 ring[kRing][V];
-  if (nT > 0) {
-    // register ring of kRing tiles, rotated by NAME (the loop is unrolled by
-    // kRing): while tile i multiplies, tiles i + 1 .. i + kRing - 1 are in
-    // flight and the wait before tile i only drains tile i's own loads.  (A
-    // rotation by register moves forces a full vmcnt(0) drain every tile:
-    // moving the youngest tile's registers waits for its loads.)
-    // issue order slot 0, 1, ... (sched barriers): the wait before the first
-    // tile then drains only slot 0's loads
+  // register ring of kRing tiles, rotated by NAME (the loop is unrolled by
+  // kRing): while tile i multiplies, tiles i + 1 .. i + kRing - 1 are in
+  // flight and the wait before tile i only drains tile i's own loads.  (A
+  // rotation by register moves forces a full vmcnt(0) drain every tile:
+  // moving the youngest tile's registers waits for its loads.)
+  // issue order slot 0, 1, ... (sched barriers): the wait before the first
+  // tile then drains only slot 0's loads.  Unconditional: under an `if (nT > 0)`
+  // the wait before the patch staging (build_A) counted only the patch loads
+  // of the no-tile path and drained two tiles of the ring.
 #pragma unroll
-    for (int k = 0; k < kRing; k++) {
-      load_tile(ring[k], k);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+  for (int k = 0; k < kRing; k++) {
+    load_tile(ring[k], k);
+    __builtin_amdgcn_sched_barrier(0);
   }
   build_A();
   // levels off the fast path (empty box, or windows too spread for it) first
@@ -569,6 +571,323 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   CORR_STAMP_RT(13);
 }
 
+// ---------------------------------------------------------------------------
+// Channel-split variant (fp32, p = 3, R = 3: DPVO's shape; EXPERIMENT, opt-in
+// with DPVO_CORR_SPLIT=1: it measured 88.8 us against the one-wave kernel's
+// 57.5 us at cfg2, see DESIGN.md §3 A-CORR round 4).  At cfg2 there are
+// 2048 edges = 2 waves per SIMD with one wave per edge, and inside a wave the
+// f32 MFMAs of a tile and the gathers of the next do not overlap well
+// (DESIGN.md §3 A-CORR diagnostics).  Here an edge is a 128-thread workgroup
+// of TWO waves, wave h owning channels [64h, 64h + 64): each wave runs half the
+// MFMAs (16 per tile) over half the bytes (4 x 16-B loads per lane per tile),
+// with half the ring registers, so the kernel fits 4 waves per SIMD and twice
+// as many independent tile streams hide each other's latency.  The two
+// partial G tiles meet in LDS through ds_add_f32 onto zero (0 + a + b rounds
+// the same in either order: deterministic); one LDS-only barrier pair per
+// level, the bilinear split by patch pixel k between the waves.
+// ---------------------------------------------------------------------------
+constexpr int kSplitThreads = 2 * kWave;
+constexpr int kSplitVecs = 4;  // 16-B loads per lane per tile (64 channels of a pixel)
+constexpr int kSplitRing = 3;
+
+__device__ __forceinline__ void wg_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__global__ void __launch_bounds__(kSplitThreads, 4)  // 4 waves per SIMD (<= 128 VGPRs)
+    corr_split_kernel(const float* __restrict__ fmap1, NhwcLevels lv, int L,
+                      const float* __restrict__ coords, const int64_t* __restrict__ ii,
+                      const int64_t* __restrict__ jj, int B, int M, int N1, int N2,
+                      const int* __restrict__ order, float* __restrict__ out) {
+  constexpr int np = 9, R = 3, D = 2 * R + 2, Dp = D - 1, nout = Dp * Dp * np;
+  constexpr int C = kNhwcC, V = kSplitVecs;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int hw = wave_uniform(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
+  float* G = smem;                                                  // [np][kBoxStride]
+  NhwcGeom* geo = reinterpret_cast<NhwcGeom*>(G + np * kBoxStride) + hw * kMaxL;  // per wave
+  float* obuf = reinterpret_cast<float*>(reinterpret_cast<NhwcGeom*>(G + np * kBoxStride) +
+                                         2 * kMaxL);                // [nout][L]
+  int edge;
+  if (order) {  // XCD-aware, as corr_nhwc_kernel (one edge per workgroup)
+    const int per = (M + 7) / 8;
+    const int p = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (p >= M) return;  // workgroup-uniform
+    edge = wave_uniform(order[p]);
+  } else {
+    edge = blockIdx.x;
+    if (edge >= B * M) return;
+  }
+  const int b = edge / M, m = edge % M;
+  const int ix = wave_uniform((int)ii[m]), jx = wave_uniform((int)jj[m]);
+  const bool idx_ok = ix >= 0 && ix < N1 && jx >= 0 && jx < N2;
+  const float cv = (lane < 2 * np) ? coords[((size_t)b * M + m) * 2 * np + lane] : 0.f;
+  __builtin_amdgcn_sched_barrier(0);
+
+  // this wave's half of the gmap patch: channels [64 hw, 64 hw + 64) x 9 =
+  // 144 16-B units, staged through the wave's own part of G (zeroed after)
+  const int ai = lane & 15, aq = lane >> 4;
+  constexpr int kUnits = 64 * np / 4, kRA = (kUnits + kWave - 1) / kWave;
+  u32x4 st[kRA];
+  {
+    const float* f1 = fmap1 + ((size_t)b * N1 + (idx_ok ? ix : 0)) * C * np + 64 * hw * np;
+#pragma unroll
+    for (int r = 0; r < kRA; r++)
+      st[r] = reinterpret_cast<const u32x4*>(f1)[min(lane + kWave * r, kUnits - 1)];
+  }
+  __builtin_amdgcn_sched_barrier(0);  // patch loads before the tile loads: their wait counts only them
+  float Af[16];  // A fragment of K step 4h + s: f1[64 hw + 16 h + 4 aq + s][ai]
+  float* stg = G + hw * (64 * np);
+  auto build_A = [&]() __attribute__((always_inline)) {
+    // unconditional: lanes past the end rewrite the last unit with its own
+    // value (a guarded store is a branch whose wait drains the tile loads)
+#pragma unroll
+    for (int r = 0; r < kRA; r++)
+      reinterpret_cast<u32x4*>(stg)[min(lane + kWave * r, kUnits - 1)] = st[r];
+    wave_lds_sync();
+    const bool arow = idx_ok && ai < np;
+#pragma unroll
+    for (int h = 0; h < 4; h++)
+#pragma unroll
+      for (int s = 0; s < 4; s++) Af[4 * h + s] = arow ? stg[(16 * h + 4 * aq + s) * np + ai] : 0.0f;
+  };
+
+  // geometry of every level (both waves, own copy: no barrier before the
+  // first tile loads)
+  int cum[kMaxL + 1];
+  {
+    const int gl = lane >> 4, gk = lane & 15;
+    const bool act = gl < L && gk < np;
+    const float xr = __shfl(cv, min(gk, np - 1), kWave), yr = __shfl(cv, np + min(gk, np - 1), kWave);
+    const float sc = LV_SEL(scale, gl < L ? gl : 0);
+    const bool pow2 = (__float_as_uint(sc) & 0x7fffffu) == 0u;
+    const float rs = 1.0f / sc;
+    const float x = pow2 ? xr * rs : xr / sc, y = pow2 ? yr * rs : yr / sc;
+    const int xf = ifloor_safe(x), yf = ifloor_safe(y);
+    if (act) {
+      geo[gl].x0[gk] = xf;
+      geo[gl].y0[gk] = yf;
+      geo[gl].dx[gk] = x - floorf(x);  // correlation_kernel.cu:262
+      geo[gl].dy[gk] = y - floorf(y);
+    }
+    int xlo = act ? xf : 0x7fffffff, ylo = act ? yf : 0x7fffffff;
+    int xhi = act ? xf : -0x7fffffff, yhi = act ? yf : -0x7fffffff;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      xlo = min(xlo, __shfl_xor(xlo, o, kWave));
+      ylo = min(ylo, __shfl_xor(ylo, o, kWave));
+      xhi = max(xhi, __shfl_xor(xhi, o, kWave));
+      yhi = max(yhi, __shfl_xor(yhi, o, kWave));
+    }
+    if (gk == 0 && gl < L) {
+      const int H2 = LV_SEL(H2, gl), W2 = LV_SEL(W2, gl);
+      xlo = max(xlo - R, 0);
+      ylo = max(ylo - R, 0);
+      xhi = min(xhi + R + 1, W2 - 1);
+      yhi = min(yhi + R + 1, H2 - 1);
+      int bw = xhi - xlo + 1, bh = yhi - ylo + 1;
+      if (bw <= 0 || bh <= 0 || !idx_ok) bw = bh = 0;
+      geo[gl].xlo = xlo;
+      geo[gl].ylo = ylo;
+      geo[gl].bw = bw;
+      geo[gl].bh = bh;
+      geo[gl].ntile = (bw * bh + 15) >> 4;
+    }
+  }
+  wave_lds_sync();
+  // level order alternates between neighbouring workgroups (fine -> coarse /
+  // coarse -> fine), so co-resident edges are not all in the same phase
+  const bool rev = (blockIdx.x >> 3) & 1;
+  auto level_at = [&](int j) { return rev ? L - 1 - j : j; };
+  cum[0] = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxL; j++) {
+    const int nt = (j < L) ? wave_uniform(geo[level_at(j)].ntile) : 0;
+    cum[j + 1] = cum[j] + ((nt <= kMaxTiles) ? nt : 0);
+  }
+  const int rx = lane >> 3, ry = lane & 7;
+  const int k0 = hw ? 5 : 0, kn = hw ? 4 : 5;  // this wave's patch pixels in the bilinear
+
+  // bilinear of level l for k in [k0, k0 + kn) (correlation_kernel.cu:260-271);
+  // fast: G holds the level's box tiles, else the raw [k][8][8] grid
+  auto bilinear = [&](int l, bool fast) __attribute__((always_inline)) {
+    const NhwcGeom* gg = geo + l;
+    const int xlo = wave_uniform(gg->xlo), ylo = wave_uniform(gg->ylo);
+    const int bw = wave_uniform(gg->bw), bh = wave_uniform(gg->bh);
+    const int cap = max(bw * bh - 1, 0);
+    float r[5], dxv[5], dyv[5];
+#pragma unroll
+    for (int u = 0; u < 5; u++) {
+      const int k = min(k0 + u, np - 1);
+      dxv[u] = gg->dx[k];
+      dyv[u] = gg->dy[k];
+      if (fast) {
+        const int gy = gg->y0[k] + ry - R - ylo, gx = gg->x0[k] + rx - R - xlo;
+        const bool in = gy >= 0 && gy < bh && gx >= 0 && gx < bw;
+        const float a = G[k * kBoxStride + min(max(gy * bw + gx, 0), cap)];
+        r[u] = in ? a : 0.f;
+      } else {
+        r[u] = G[k * 64 + ry * 8 + rx];
+      }
+    }
+    float v[5];
+#pragma unroll
+    for (int u = 0; u < 5; u++) {
+      const float r10 = __shfl_down(r[u], 1, kWave);
+      const float r01 = __shfl_down(r[u], 8, kWave);
+      const float r11 = __shfl_down(r[u], 9, kWave);
+      const float dx = dxv[u], dy = dyv[u];
+      float t = ((1.f - dx) * (1.f - dy)) * r[u];
+      t = t + (dx * (1.f - dy)) * r01;
+      t = t + ((1.f - dx) * dy) * r10;
+      t = t + (dx * dy) * r11;
+      v[u] = t;
+    }
+    if (rx < 7 && ry < 7) {
+#pragma unroll
+      for (int u = 0; u < 5; u++)
+        if (u < kn) obuf[((rx * 7 + ry) * 9 + k0 + u) * L + l] = v[u];
+    }
+  };
+  // zero this wave's rows of G over n entries per row
+  auto zero_rows = [&](int n, int stride) __attribute__((always_inline)) {
+    for (int u = 0; u < kn; u++)
+      for (int e = lane; e < n; e += kWave) G[(k0 + u) * stride + e] = 0.f;
+  };
+
+  const int nT = cum[kMaxL];
+  const float* pbase[kMaxL];
+  int prow[kMaxL], pbw[kMaxL], pnpx[kMaxL];
+  float prbw[kMaxL];
+#pragma unroll
+  for (int j = 0; j < kMaxL; j++) {
+    const int l = (j < L) ? level_at(j) : 0;
+    const NhwcGeom* gg = geo + l;
+    const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
+    const int bw0 = max(wave_uniform(gg->bw), 1);
+    pbw[j] = bw0;
+    pnpx[j] = bw0 * wave_uniform(gg->bh);
+    prbw[j] = 1.0f / (float)bw0;
+    prow[j] = W2 * C;
+    // an empty box reads the frame's first pixel (in range whatever the
+    // coordinates): the ring preload below is then unconditional
+    const bool empty = wave_uniform(gg->bw) <= 0 || wave_uniform(gg->bh) <= 0;
+    pbase[j] = static_cast<const float*>(LV_SEL(f2, l)) +
+               (((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 +
+                (empty ? 0 : (size_t)wave_uniform(gg->ylo) * W2 + wave_uniform(gg->xlo))) * C +
+               64 * hw;
+  }
+  auto pick = [](int j, auto a0, auto a1, auto a2, auto a3) __attribute__((always_inline)) {
+    return j == 0 ? a0 : j == 1 ? a1 : j == 2 ? a2 : a3;
+  };
+  auto load_tile = [&](u32x4 (&dst)[V], int i) __attribute__((always_inline)) {
+    i = min(i, max(nT - 1, 0));
+    const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
+    const int t = i - pick(j, 0, cum[1], cum[2], cum[3]);
+    const float* base = pick(j, pbase[0], pbase[1], pbase[2], pbase[3]);
+    const int row = pick(j, prow[0], prow[1], prow[2], prow[3]);
+    const int bw0 = pick(j, pbw[0], pbw[1], pbw[2], pbw[3]);
+    const int npx = pick(j, pnpx[0], pnpx[1], pnpx[2], pnpx[3]);
+    const float rbw = pick(j, prbw[0], prbw[1], prbw[2], prbw[3]);
+    const int px = min(16 * t + ai, max(npx - 1, 0));
+    const int rr = (int)(((float)px + 0.5f) * rbw), cc = px - rr * bw0;
+    const float* s = base + rr * row + cc * C + 4 * aq;
+#pragma unroll
+    for (int h = 0; h < V; h++) dst[h] = *reinterpret_cast<const u32x4*>(s + 16 * h);
+  };
+  // unconditional (a branch here makes the wait before the patch staging
+  // count only the patch loads on the no-tile path: it would drain the ring)
+  u32x4 ring[kSplitRing][V];
+#pragma unroll
+  for (int k = 0; k < kSplitRing; k++) {
+    load_tile(ring[k], k);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  build_A();
+  // G holds the other wave's staging until here
+  wg_lds_sync();
+  zero_rows(kBoxStride, kBoxStride);
+  wg_lds_sync();
+  // levels off the fast path first (raw grid straight into G, full channel sums)
+  for (int l = 0; l < L; l++) {
+    const int nt = wave_uniform(geo[l].ntile);
+    if (nt > kMaxTiles) {
+      const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
+      const float* f2 = static_cast<const float*>(LV_SEL(f2, l)) + ((size_t)b * N2 + jx) * H2 * W2 * C;
+      for (int e = threadIdx.x; e < np * D * D; e += kSplitThreads) {
+        const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
+        const int i1 = geo[l].y0[k] + yy - R, j1 = geo[l].x0[k] + xx - R;
+        float sacc = 0.f;
+        if (idx_ok && i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
+          const float* px = f2 + ((size_t)i1 * W2 + j1) * C;
+          const float* f1 = fmap1 + ((size_t)b * N1 + ix) * C * np;
+          for (int c = 0; c < C; c++) sacc += f1[(size_t)c * np + k] * px[c];
+        }
+        G[e] = sacc;
+      }
+      wg_lds_sync();
+      bilinear(l, false);
+      wg_lds_sync();
+      zero_rows(D * D, D * D);
+      wg_lds_sync();
+    } else if (nt == 0) {
+      bilinear(l, true);
+    }
+  }
+  if (nT > 0) {
+    auto step = [&](u32x4 (&cur)[V], int i) __attribute__((always_inline)) {
+      const bool live = i < nT;
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      if (live) {
+#pragma unroll
+        for (int h = 0; h < V; h += 2) {
+          const float4 c0 = __builtin_bit_cast(float4, cur[h]);
+          const float4 c1 = __builtin_bit_cast(float4, cur[h + 1]);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 0], c0.x, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 4], c1.x, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 1], c0.y, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 5], c1.y, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 2], c0.z, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 6], c1.z, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 3], c0.w, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 7], c1.w, acc1, 0, 0, 0);
+        }
+      }
+      load_tile(cur, i + kSplitRing);
+      if (!live) return;
+      const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
+      const int t = i - pick(j, 0, cum[1], cum[2], cum[3]), l = level_at(j);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = 4 * aq + r;
+        if (row < np) atomicAdd(&G[row * kBoxStride + 16 * t + ai], acc0[r] + acc1[r]);
+      }
+      const int le = pick(j, cum[1], cum[2], cum[3], cum[4]);
+      if (i + 1 == le) {  // level complete in both waves: bilinear, then G zero again
+        wg_lds_sync();
+        bilinear(l, true);
+        wg_lds_sync();
+        zero_rows(16 * (le - pick(j, 0, cum[1], cum[2], cum[3])), kBoxStride);
+        wg_lds_sync();
+      }
+    };
+    for (int i = 0; i < nT; i += kSplitRing) {
+#pragma unroll
+      for (int k = 0; k < kSplitRing; k++) step(ring[k], i + k);
+    }
+  }
+  // ---- one contiguous [nout][L] row block per edge, both waves
+  wg_lds_sync();
+  float* dst = out + ((size_t)b * M + m) * nout * L;
+  if (((nout * L) & 3) == 0) {
+    for (int e = 4 * (int)threadIdx.x; e < nout * L; e += 4 * kSplitThreads)
+      *reinterpret_cast<float4*>(dst + e) = *reinterpret_cast<const float4*>(obuf + e);
+  } else {
+    for (int e = threadIdx.x; e < nout * L; e += kSplitThreads) dst[e] = obuf[e];
+  }
+}
+
 // [count, C, H, W] -> [count, H, W, C] (one 32 x 32 tile of (c, hw) per block)
 template <typename T>
 __global__ void __launch_bounds__(256)
@@ -613,6 +932,14 @@ __global__ void __launch_bounds__(256)
 
 using namespace dpvo;
 
+// DPVO_CORR_SPLIT=1 selects the channel-split kernel for fp32 (experiment, off:
+// 88.8 us against 57.5 us for the one-wave-per-edge kernel at cfg2,
+// profiles/r04_corr_split/)
+static bool corr_split_enabled() {
+  static const char* ov = getenv("DPVO_CORR_SPLIT");
+  return ov && ov[0] == '1';
+}
+
 DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
     const void* fmap1, const void* const* fmap2, const int* H2, const int* W2, const float* scale,
     int L, const float* coords, const int64_t* ii, const int64_t* jj, const int32_t* order, int B,
@@ -647,6 +974,16 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   const bool raw9 = np == 9 && radius == 3;  // DPVO: p = 3, R = 3
   const dim3 g(grid), blk(kNhwcWaves * kWave);
   hipStream_t st = as_stream(stream);
+  if (dtype == DPVO_F32 && raw9 && corr_split_enabled()) {
+    // one edge per 128-thread workgroup (channel-split waves)
+    unsigned g2 = (unsigned)units;
+    if (ordered) g2 = 8u * (unsigned)((g2 + 7) / 8);
+    const size_t smem2 = sizeof(float) * np * kBoxStride + sizeof(NhwcGeom) * 2 * kMaxL +
+                         sizeof(float) * corr_obuf_floats(np, radius, L);
+    hipLaunchKernelGGL(corr_split_kernel, dim3(g2), dim3(kSplitThreads), smem2, st,
+                       (const float*)fmap1, lv, L, coords, ii, jj, B, M, N1, N2, ord, out);
+    return launch_status();
+  }
   if (dtype == DPVO_F16) {
     const __half* f1 = (const __half*)fmap1;
     if (raw9)

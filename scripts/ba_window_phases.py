@@ -65,6 +65,12 @@ for k, v in acc.items():
     v = sorted(v)
     print(f"{k:34s} median {v[len(v) // 2]:8.2f} us")
 
+# dense kernel (DPVO_BA_DENSE=1): workgroup 0's pass 0 of iteration 0
+if m[55] and m[58]:
+    print(f"dense wg0 pass0: (1) linearise {(m[56] - m[55]) * 0.01:.2f} us, (2) slots "
+          f"{(m[57] - m[56]) * 0.01:.2f} us, (3) block items {(m[58] - m[57]) * 0.01:.2f} us; "
+          f"passes {m[59]}, own edges {m[60]}, own patches {m[61]}")
+
 # per-workgroup spread (window kernel stamps [128 + 256 it + g] assembled,
 # [640 + 256 it + g] every partial seen), last call
 if m[128] and len(m) >= 1664:

@@ -3,7 +3,7 @@ HIP-event medians at cfg2 (and a DPVO window) of the fused frame insertion +
 reprojection + A-CORR edge order + BA plan launch against its parts run
 alone -- reproject (+ order), the plan kernel, the pyramid insertion.
 
-    python scripts/reproject_launch_bench.py
+    python scripts/reproject_launch_bench.py [cfg2|dpvo25 ...]
 """
 import json
 import os
@@ -38,7 +38,7 @@ def main():
     mem, levels = 36, (1, 2, 4, 8)
     pyr_nchw = synthetic.make_features(mem=mem, C=128, levels=levels, seed=0, device=dev)
     pyr = [synthetic.channels_last(p) for p in pyr_nchw]
-    for name in ("cfg2", "dpvo25"):
+    for name in (sys.argv[1:] or ["cfg2", "dpvo25"]):
         if name == "cfg2":
             G = synthetic.make_config("cfg2", seed=0)
             t0, t1 = 1, G.F
