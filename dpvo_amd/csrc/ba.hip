@@ -43,7 +43,7 @@ constexpr int kMaxFree = 20;  // pose-block masks are 32-bit; lower S blocks of 
 constexpr int kPerThread = kMaxSetupE / kSetupThreads;
 constexpr int kCtlBytes = 512;
 constexpr int kSetupLds = 160 * 1024;
-constexpr int kMarks = 1664;  // [0, 128) phases; window kernel per workgroup: [128 + 256 it + g] assembled, [640 + 256 it + g] all partials seen, [1152 + g] setup, [1408 + g] it 0 pre-reduction
+constexpr int kMarks = 2176;  // [0, 128) phases; window kernel per workgroup: [128 + 256 it + g] assembled, [640 + 256 it + g] all partials seen, [1152 + g] setup, [1408 + g] it 0 pre-reduction; dense kernel: [1664 + g] it 0 linearised, [1920 + g] own edges | patches << 16
 constexpr int kNoPose = 31;
 constexpr int kEC = 16;  // doubles per position record of E terms
 

@@ -35,7 +35,10 @@ __device__ inline int fscan(int* data, int n, int* scr, int pack_shift = 0) {
     const int lo = base + min(tid * cper, cn), hi = base + min(tid * cper + cper, cn);
     int v[kScanRun];
 #pragma unroll
-    for (int k = 0; k < kScanRun; k++) v[k] = (lo + k < hi) ? data[lo + k] : 0;
+    for (int k = 0; k < kScanRun; k++) {  // unconditional read, then select (no branch per load)
+      const int d = data[min(lo + k, n - 1)];
+      v[k] = (lo + k < hi) ? d : 0;
+    }
     if (pack_shift > 0) {
 #pragma unroll
       for (int k = 0; k < kScanRun; k++) v[k] = (v[k] << pack_shift) | (v[k] > 0 ? 1 : 0);
@@ -43,23 +46,15 @@ __device__ inline int fscan(int* data, int n, int* scr, int pack_shift = 0) {
     int s = 0;
 #pragma unroll
     for (int k = 0; k < kScanRun; k++) s += v[k];
-    const int lane = tid & 63, wid = tid >> 6;
-    int x = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int t = __shfl_up(x, o, 64);
-      if (lane >= o) x += t;
-    }
+    const int lane = tid & 63, wid = tid >> 6, nw = nt / 64;
+    const int x = wave_incl_sum(s);  // DPP: no LDS round trip per step
     if (lane == 63) scr[wid] = x;
     __syncthreads();
-    if (tid == 0) {
-      int acc = 0;
-      for (int w = 0; w < nt / 64; w++) {
-        const int y = scr[w];
-        scr[w] = acc;
-        acc += y;
-      }
-      scr[nt / 64] = acc;
+    if (wid == 0) {  // exclusive prefix of the (<= 16) wave totals, one DPP scan
+      const int y = lane < nw ? scr[lane] : 0;
+      const int inc = wave_incl_sum(y);
+      if (lane < nw) scr[lane] = inc - y;
+      if (lane == nw - 1) scr[nw] = inc;
     }
     __syncthreads();
     int run = total + scr[wid] + x - s;

@@ -103,7 +103,7 @@ struct WArgs {
   float* ejg;        // [2][E][12] E entries by edge and iteration parity (fp32), HBM fallback
   int* status;       // [1] OR of status bits (workspace meta)
   int* sink;         // caller's sticky status word (dpvo_ba_set_status_sink) or null
-  int64_t* marks;    // [1664] wall-clock stamps (instrumentation, dpvo_ba_set_marks): [0, 64)
+  int64_t* marks;    // [2176] wall-clock stamps (instrumentation, dpvo_ba_set_marks): [0, 64)
                      // phases of workgroup 0, [128 + 256 it + g] / [640 + 256 it + g] per
                      // workgroup assembled / all partials seen, [1152 + g] setup done,
                      // [1408 + g] iteration 0 assembled (before the reduction); null on
@@ -236,13 +236,10 @@ __device__ __forceinline__ void plan_edges_pass(const int64_t* __restrict__ ii,
       }
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    kmin = min(kmin, __shfl_xor(kmin, o, 64));
-    kmax = max(kmax, __shfl_xor(kmax, o, 64));
-    fmin = min(fmin, __shfl_xor(fmin, o, 64));
-    bad |= __shfl_xor(bad, o, 64);
-  }
+  kmin = wave_min_i(kmin);
+  kmax = wave_max_i(kmax);
+  fmin = wave_min_i(fmin);
+  bad = wave_max_i(bad);
   if (lane == 0) {
     atomicMin(&ctl[0], kmin);
     atomicMax(&ctl[1], kmax);
@@ -506,6 +503,13 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
     return;
   }
   if (plan.t0d) t0 = *plan.t0d;
+  // phase stamps of shard 0 (100 MHz wall clock, 8 stores per launch):
+  // meta + 16 as int64 [6] (scripts/plan_phases.py)
+  auto stamp = [&](int q) {
+    if (s == 0 && threadIdx.x == 0)
+      reinterpret_cast<int64_t*>(plan.meta + 16)[q] = (int64_t)wall_clock64();
+  };
+  stamp(0);
   //   [ctl 256 B | code u16[cap] | spos u16[cap] | pres u32[kHistMax / 32] | hist int[nl] | pm u32[nl]]
   const int tid = threadIdx.x, lane = tid & 63, T = kPT;
   int* ctl = (int*)lds;  // [0..3] as plan_edges_pass, [4] below, [5] ubelow, [6] nuniq
@@ -516,6 +520,7 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
   int* hist = reinterpret_cast<int*>(pres + kHistMax / 32);
   int kv[kPlanPer];
   plan_edges_pass(ii, jj, kk, E, num_patches, num_poses, t0, N, ctl, code, kv);
+  stamp(1);
   const int kmin = ctl[0], R = ctl[1] - kmin + 1;
   const int nlmax = (R + S - 1) / S;
   const bool fits = E > 0 && R <= kHistMax && E < (1 << 14) &&
@@ -552,6 +557,7 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
     else if (v < hi) atomicAdd(&hist[v - lo], 1);
   }
   __syncthreads();  // presence bitmap complete
+  stamp(2);
   int ub = 0, nu = 0;
   for (int w = tid; w < nw; w += T) {
     const unsigned x = pres[w];
@@ -559,12 +565,9 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
     nu += __popc(x);
     ub += (b0 + 32 <= lo) ? __popc(x) : (b0 < lo ? __popc(x & ((1u << (lo - b0)) - 1u)) : 0);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    nb += __shfl_xor(nb, o, 64);
-    ub += __shfl_xor(ub, o, 64);
-    nu += __shfl_xor(nu, o, 64);
-  }
+  nb = wave_sum_i(nb);
+  ub = wave_sum_i(ub);
+  nu = wave_sum_i(nu);
   if (lane == 0) {
     atomicAdd(&ctl[4], nb);
     atomicAdd(&ctl[5], ub);
@@ -573,6 +576,7 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
   // local counting sort in one packed scan (plan_block's fast path); the
   // scan's barriers also complete the ctl sums above
   fscan(hist, nl, scr, 14);
+  stamp(3);
   const int below = ctl[4], ubelow = ctl[5], nuniq = ctl[6];
 #pragma unroll
   for (int r = 0; r < kPlanPer; r++) {
@@ -586,6 +590,7 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
     if (m) atomicOr(&pm[old & 0x3fff], m);
   }
   __syncthreads();
+  stamp(4);
 #pragma unroll
   for (int r = 0; r < kPlanPer; r++) {
     const int e = tid + r * T;
@@ -610,6 +615,7 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
     if (ctl[3] && plan.sink) atomicOr(plan.sink, ctl[3]);
     *plan.status = 0;
   }
+  stamp(5);
 }
 
 __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict__ ii,
@@ -749,6 +755,45 @@ struct WL {  // LDS layout of one workgroup
 };
 
 enum { cNrel = 0, cNrp = 1, cFmin = 2, cFail = 3, cTimeout = 4, cCap = 5, cFailAny = 6, cScan = 16 };
+
+// E^T dX of relevant patch ri (ba_cuda.cu:563), its edges in order.  The E
+// entries of kEb edges (HBM sc1 loads on the fallback path) and the dX rows
+// they pair with are all read before the first is used, with clamped indices
+// and selects instead of guarded reads: one round trip per kEb edges, not one
+// per edge (the per-edge loop made the final apply at E = 9850 a chain of
+// dependent HBM loads, 12.6 us).  Adding +0.0 for an absent term leaves ex
+// unchanged, so the sum is the one of the per-edge loop.
+__device__ __forceinline__ double patch_etdx(const WL& L, const WArgs& A, int ri, int par, int N) {
+  constexpr int kEb = 4;
+  double ex = 0.0;
+  const int q0 = L.roff[ri], q1 = L.roff[ri + 1];
+  for (int qb = q0; qb < q1; qb += kEb) {
+    float4 e[kEb][3];
+    unsigned cc[kEb];
+#pragma unroll
+    for (int u = 0; u < kEb; u++) {
+      const int q = min(qb + u, q1 - 1);
+      cc[u] = L.ec[q];
+      L.ld_ej(A.ejg, A.E, q, par, e[u][0], e[u][1], e[u][2]);
+    }
+#pragma unroll
+    for (int u = 0; u < kEb; u++) {
+      const bool live = qb + u < q1;
+      const unsigned si = cc[u] & 0xff, sj = cc[u] >> 8;
+      const unsigned nm = (unsigned)max(N - 1, 0);
+      const double* dj = L.dX + 6 * min(sj, nm);
+      const double* di = L.dX + 6 * min(si, nm);
+      const float4 e0 = e[u][0], e1 = e[u][1], e2 = e[u][2];
+      const double tj = (double)e0.x * dj[0] + (double)e0.y * dj[1] + (double)e0.z * dj[2] +
+                        (double)e0.w * dj[3] + (double)e1.x * dj[4] + (double)e1.y * dj[5];
+      const double ti = (double)e1.z * di[0] + (double)e1.w * di[1] + (double)e2.x * di[2] +
+                        (double)e2.y * di[3] + (double)e2.z * di[4] + (double)e2.w * di[5];
+      ex += (live && sj < (unsigned)N) ? tj : 0.0;
+      ex += (live && si < (unsigned)N) ? ti : 0.0;
+    }
+  }
+  return ex;
+}
 
 __device__ __forceinline__ unsigned wslot(int gp, int t0, int N, int fmin) {
   if (gp >= t0 && gp < t0 + N) return (unsigned)(gp - t0);
@@ -1324,23 +1369,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
         pl[3] = q1[0]; pl[4] = q1[1]; pl[5] = q1[2]; pl[6] = q1[3];
       }
       for (int ri = tid; ri < nrel_e; ri += kWT) {  // dZ = Q (u - E^T dX) (:563), patch_retr (:209-229)
-        double ex = 0.0;
-        for (int q = L.roff[ri]; q < L.roff[ri + 1]; q++) {
-          const unsigned c = L.ec[q];
-          const unsigned si = c & 0xff, sj = c >> 8;
-          float4 e0, e1, e2;
-          L.ld_ej(A.ejg, A.E, q, (it - 1) & 1, e0, e1, e2);
-          if (sj < (unsigned)N) {
-            const double* d = L.dX + 6 * sj;
-            ex += (double)e0.x * d[0] + (double)e0.y * d[1] + (double)e0.z * d[2] +
-                  (double)e0.w * d[3] + (double)e1.x * d[4] + (double)e1.y * d[5];
-          }
-          if (si < (unsigned)N) {
-            const double* d = L.dX + 6 * si;
-            ex += (double)e1.z * d[0] + (double)e1.w * d[1] + (double)e2.x * d[2] +
-                  (double)e2.y * d[3] + (double)e2.z * d[4] + (double)e2.w * d[5];
-          }
-        }
+        const double ex = patch_etdx(L, A, ri, (it - 1) & 1, N);
         const double2 qu = L.qu[ri];
         const float dz = (float)(qu.x * (qu.y - ex));
         const float base = (it == 1) ? L.dbase[ri] : L.dep[ri];
@@ -1595,23 +1624,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     }
     for (int ri = tid; ri < nrel_e; ri += kWT) {
       if (L.pkx[ri] < 0) continue;
-      double ex = 0.0;
-      for (int q = L.roff[ri]; q < L.roff[ri + 1]; q++) {
-        const unsigned c = L.ec[q];
-        const unsigned si = c & 0xff, sj = c >> 8;
-        float4 e0, e1, e2;
-        L.ld_ej(A.ejg, A.E, q, (it - 1) & 1, e0, e1, e2);
-        if (sj < (unsigned)N) {
-          const double* d = L.dX + 6 * sj;
-          ex += (double)e0.x * d[0] + (double)e0.y * d[1] + (double)e0.z * d[2] +
-                (double)e0.w * d[3] + (double)e1.x * d[4] + (double)e1.y * d[5];
-        }
-        if (si < (unsigned)N) {
-          const double* d = L.dX + 6 * si;
-          ex += (double)e1.z * d[0] + (double)e1.w * d[1] + (double)e2.x * d[2] +
-                (double)e2.y * d[3] + (double)e2.z * d[4] + (double)e2.w * d[5];
-        }
-      }
+      const double ex = patch_etdx(L, A, ri, (it - 1) & 1, N);
       const double2 qu = L.qu[ri];
       const float dz = (float)(qu.x * (qu.y - ex));
       const float base = (it == 1) ? L.dbase[ri] : L.dep[ri];
@@ -1951,6 +1964,10 @@ __global__ void __launch_bounds__(kWT) ba_dense_kernel(WArgs A) {
       }
       __syncthreads();
       if (it == 0 && pa == 0) mark(A, 56);  // diagnostics: pass 0 sub-stages of workgroup 0
+      if (it == 0 && pa == 0 && A.marks && tid == 0 && g < 256) {
+        A.marks[1664 + g] = (int64_t)wall_clock64();
+        A.marks[1920 + g] = (int64_t)D.ne | ((int64_t)D.np << 16);
+      }
       // (2) thread per (own patch, slot): C, u (slot 0) and the E column block at
       // the slot's pose, edges in order (fp64 products of the fp32 terms)
       {
@@ -2446,7 +2463,8 @@ void ba_window_plan_offsets(int E, int64_t* out) {
   out[1] = out[0] + (int64_t)al256w(sizeof(int) * (size_t)E);  // poff [E + 1]
   out[2] = out[1] + (int64_t)al256w(sizeof(int) * (size_t)(E + 1));  // pmask [E]
   out[3] = out[2] + (int64_t)al256w(sizeof(unsigned) * (size_t)E);  // pkk [E]
-  out[4] = out[3] + (int64_t)al256w(sizeof(int) * (size_t)E);  // meta [8]: nuniq, fmin, status
+  out[4] = out[3] + (int64_t)al256w(sizeof(int) * (size_t)E);  // meta [8]: nuniq, fmin, status;
+                                                               // [16, 28): int64 phase stamps
 }
 
 static Plan plan_view(char* scratch, int E, int* status) {

@@ -61,6 +61,36 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// wave64 inclusive scan of ints with DPP (row shifts 1/2/4/8 inside each row
+// of 16 lanes, then row_bcast:15 / row_bcast:31 across rows): six VALU ops
+// with a DPP source.  A __shfl_* is a ds_bpermute, an LDS round trip per
+// step.  `id` is op's identity (what an out-of-row source contributes).
+template <typename Op>
+__device__ __forceinline__ int wave_scan_dpp(int x, int id, Op op) {
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x114, 0xf, 0xf, false));  // row_shr:4
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x118, 0xf, 0xf, false));  // row_shr:8
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  x = op(x, __builtin_amdgcn_update_dpp(id, x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return x;
+}
+__device__ __forceinline__ int wave_incl_sum(int x) {
+  return wave_scan_dpp(x, 0, [](int a, int b) { return a + b; });
+}
+// wave-wide reductions (every lane gets the result)
+__device__ __forceinline__ int wave_sum_i(int x) {
+  return __builtin_amdgcn_readlane(wave_incl_sum(x), 63);
+}
+__device__ __forceinline__ int wave_min_i(int x) {
+  return __builtin_amdgcn_readlane(
+      wave_scan_dpp(x, 0x7fffffff, [](int a, int b) { return a < b ? a : b; }), 63);
+}
+__device__ __forceinline__ int wave_max_i(int x) {
+  return __builtin_amdgcn_readlane(
+      wave_scan_dpp(x, (int)0x80000000, [](int a, int b) { return a > b ? a : b; }), 63);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

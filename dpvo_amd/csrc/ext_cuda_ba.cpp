@@ -253,7 +253,7 @@ void ba_forward_planned(torch::Tensor ws, torch::Tensor poses, torch::Tensor pat
   track_status(ws, poses, E, t0, t1);
 }
 
-// Same call; returns the 1664 phase marks (100 MHz ticks: [0, 128) phases; window kernel
+// Same call; returns the 2176 phase marks (100 MHz ticks: [0, 128) phases; window kernel
 // [128 + 256 it + g] / [640 + 256 it + g] per-workgroup assembled / partials seen, [1152 + g]
 // setup done, [1408 + g] iteration 0 assembled before its reduction) followed by the
 // multi-kernel path's per-workgroup marks.
@@ -272,7 +272,7 @@ torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
     throw;
   }
   check_status(dpvo_ba_set_marks(0), "cuda_ba.forward_marks");
-  auto out = torch::zeros({1664}, poses.options().dtype(torch::kInt64));
+  auto out = torch::zeros({2176}, poses.options().dtype(torch::kInt64));
   if (!ws.defined()) return out;
   check_status(dpvo_ba_phase_marks(ws.data_ptr(), ii.numel(), t0, t1, out.data_ptr<int64_t>(),
                                    current_stream()),

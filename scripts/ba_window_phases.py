@@ -89,6 +89,12 @@ if m[128] and len(m) >= 1664:
     print(f"setup done at {min(setup):.2f}..{max(setup):.2f} us (median "
           f"{statistics.median(setup):.2f}); it0 pre-reduction at {min(pre):.2f}..{max(pre):.2f} "
           f"(median {statistics.median(pre):.2f})")
+    if len(m) >= 2176 and m[1664]:  # dense kernel: linearised (pass 0) + own edges / patches
+        info = [(g, m[1920 + g] & 0xffff, m[1920 + g] >> 16,
+                 round((m[1664 + g] - m[1152 + g]) * 0.01, 2),
+                 round((m[1408 + g] - m[1664 + g]) * 0.01, 2)) for g in order[-8:] + order[:3]]
+        print("dense (g: own edges, own patches, setup->linearised us, linearised->pre-reduce us), "
+              "slowest 8 then fastest 3:", info)
     print("per workgroup (g: setup, pre-reduce, assembled, seen):",
           [(g, round(setup[g], 2), round(pre[g], 2), round((m[128 + g] - m[0]) * 0.01, 2),
             round((m[640 + g] - m[0]) * 0.01, 2)) for g in order[-8:]])

@@ -7,6 +7,8 @@
 // the max |A A^-1 - I|.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -I dpvo_amd/csrc \
 //         scripts/micro/bgj_bench.hip -o scripts/micro/bgj_bench
+// (add -DBGJ_THREAD_PIVOT for the per-thread pivot-solve variant; results in
+// profiles/r04_cfg4_bgj_phases.txt)
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
