@@ -27,6 +27,38 @@ constexpr int kScanRun = 16;
 // of nonzero entries before (low bits) -- bucket starts and bucket indices.
 __device__ inline int fscan(int* data, int n, int* scr, int pack_shift = 0) {
   const int tid = threadIdx.x, nt = blockDim.x;
+  if (n <= 0) return 0;
+  if (n <= 64 * kScanRun) {
+    // small scans (the plan's shard ranges, the BA setup's patch counts at
+    // cfg2): wave 0 alone, one DPP scan, two barriers instead of three
+    if (tid < 64) {
+      const int per = (n + 63) / 64;
+      const int lo = min(tid * per, n), hi = min(lo + per, n);
+      int v[kScanRun];
+#pragma unroll
+      for (int k = 0; k < kScanRun; k++) {
+        const int d = data[min(lo + k, max(n - 1, 0))];
+        v[k] = (lo + k < hi) ? d : 0;
+        if (pack_shift > 0) v[k] = (v[k] << pack_shift) | (v[k] > 0 ? 1 : 0);
+      }
+      int sum = 0;
+#pragma unroll
+      for (int k = 0; k < kScanRun; k++) sum += v[k];
+      const int x = wave_incl_sum(sum);
+      int run = x - sum;
+#pragma unroll
+      for (int k = 0; k < kScanRun; k++)
+        if (lo + k < hi) {
+          data[lo + k] = run;
+          run += v[k];
+        }
+      if (tid == 63) scr[0] = x;
+    }
+    __syncthreads();
+    const int total = scr[0];
+    __syncthreads();  // scr[0] read everywhere before the next scan writes it
+    return total;
+  }
   const int per = (n + nt - 1) / nt;
   int total = 0;
   for (int base = 0; base < n; base += nt * kScanRun) {  // chunks of nt * kScanRun

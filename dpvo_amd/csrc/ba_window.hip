@@ -510,21 +510,20 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
       reinterpret_cast<int64_t*>(plan.meta + 16)[q] = (int64_t)wall_clock64();
   };
   stamp(0);
-  //   [ctl 256 B | code u16[cap] | spos u16[cap] | pres u32[kHistMax / 32] | hist int[nl] | pm u32[nl]]
+  //   [ctl 256 B | code u16[cap] | spos u16[cap] | hf int[R] | pm u32[nl]]
   const int tid = threadIdx.x, lane = tid & 63, T = kPT;
   int* ctl = (int*)lds;  // [0..3] as plan_edges_pass, [4] below, [5] ubelow, [6] nuniq
   int* scr = ctl + 16;
   unsigned short* code = (unsigned short*)(lds + 256);
   unsigned short* spos = code + cap;
-  unsigned* pres = reinterpret_cast<unsigned*>(spos + cap);
-  int* hist = reinterpret_cast<int*>(pres + kHistMax / 32);
+  int* hf = reinterpret_cast<int*>(spos + cap);  // histogram of kk - kmin over the FULL range
   int kv[kPlanPer];
   plan_edges_pass(ii, jj, kk, E, num_patches, num_poses, t0, N, ctl, code, kv);
   stamp(1);
   const int kmin = ctl[0], R = ctl[1] - kmin + 1;
   const int nlmax = (R + S - 1) / S;
   const bool fits = E > 0 && R <= kHistMax && E < (1 << 14) &&
-                    256 + 4 * (size_t)cap + 4 * (size_t)(kHistMax / 32) + 8 * (size_t)nlmax <= lds_bytes;
+                    256 + 4 * (size_t)cap + 4 * (size_t)R + 4 * (size_t)nlmax <= lds_bytes;
   if (!fits) {  // shard-uniform (every shard saw the same edges)
     if (s == 0) {
       __syncthreads();  // ctl is re-initialised by plan_block
@@ -533,37 +532,35 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
     return;
   }
   const int lo = (int)((long long)R * s / S), hi = (int)((long long)R * (s + 1) / S), nl = hi - lo;
-  unsigned* pm = reinterpret_cast<unsigned*>(hist + nl);
-  const int nw = (R + 31) >> 5;
-  for (int w = tid; w < nw; w += T) pres[w] = 0u;
-  for (int v = tid; v < nl; v += T) {
-    hist[v] = 0;
-    pm[v] = 0u;
-  }
+  unsigned* pm = reinterpret_cast<unsigned*>(hf + R);
+  for (int v = tid; v < R; v += T) hf[v] = 0;
+  for (int v = tid; v < nl; v += T) pm[v] = 0u;
   if (tid == 0) {
     ctl[4] = 0;
     ctl[5] = 0;
     ctl[6] = 0;
   }
   __syncthreads();
+  // one histogram of the whole kk range: its nonzero buckets below lo number
+  // the patches before this shard's, and its [lo, hi) slice is the local
+  // counting sort's input (a patch's ~4-10 edges share a bucket; a presence
+  // bitmap word took 32 patches' worth of atomics)
   int nb = 0;
 #pragma unroll
   for (int r = 0; r < kPlanPer; r++) {
     const int e = tid + r * T;
     if (e >= E) continue;
     const int v = kv[r] - kmin;
-    atomicOr(&pres[v >> 5], 1u << (v & 31));
-    if (v < lo) nb++;
-    else if (v < hi) atomicAdd(&hist[v - lo], 1);
+    atomicAdd(&hf[v], 1);
+    nb += v < lo ? 1 : 0;
   }
-  __syncthreads();  // presence bitmap complete
+  __syncthreads();  // histogram complete
   stamp(2);
   int ub = 0, nu = 0;
-  for (int w = tid; w < nw; w += T) {
-    const unsigned x = pres[w];
-    const int b0 = 32 * w;
-    nu += __popc(x);
-    ub += (b0 + 32 <= lo) ? __popc(x) : (b0 < lo ? __popc(x & ((1u << (lo - b0)) - 1u)) : 0);
+  for (int v = tid; v < R; v += T) {
+    const int present = hf[v] > 0 ? 1 : 0;
+    nu += present;
+    ub += v < lo ? present : 0;
   }
   nb = wave_sum_i(nb);
   ub = wave_sum_i(ub);
@@ -573,6 +570,7 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
     atomicAdd(&ctl[5], ub);
     atomicAdd(&ctl[6], nu);
   }
+  int* hist = hf + lo;  // this shard's buckets
   // local counting sort in one packed scan (plan_block's fast path); the
   // scan's barriers also complete the ctl sums above
   fscan(hist, nl, scr, 14);

@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 O=gpurun_out
-T=r04p
+T=r04q
 run() { name=$1; shift; timeout -k 10 300 "$@" > $O/${T}_$name.txt 2>&1 || { cat $O/${T}_$name.txt; exit 1; }; tail -6 $O/${T}_$name.txt; }
 run plan_phases python -u scripts/plan_phases.py
 run phases_dpvo25_block python -u scripts/ba_window_phases.py 25 1
