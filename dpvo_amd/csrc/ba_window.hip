@@ -754,17 +754,18 @@ struct WL {  // LDS layout of one workgroup
 
 enum { cNrel = 0, cNrp = 1, cFmin = 2, cFail = 3, cTimeout = 4, cCap = 5, cFailAny = 6, cScan = 16 };
 
-// E^T dX of relevant patch ri (ba_cuda.cu:563), its edges in order.  The E
+// E^T dX over relevant edges [q0, q1) (ba_cuda.cu:563), in order (patch_etdx:
+// all edges of relevant patch ri).  The E
 // entries of kEb edges (HBM sc1 loads on the fallback path) and the dX rows
 // they pair with are all read before the first is used, with clamped indices
 // and selects instead of guarded reads: one round trip per kEb edges, not one
 // per edge (the per-edge loop made the final apply at E = 9850 a chain of
 // dependent HBM loads, 12.6 us).  Adding +0.0 for an absent term leaves ex
 // unchanged, so the sum is the one of the per-edge loop.
-__device__ __forceinline__ double patch_etdx(const WL& L, const WArgs& A, int ri, int par, int N) {
+__device__ __forceinline__ double edges_etdx(const WL& L, const WArgs& A, int q0, int q1, int par,
+                                             int N) {
   constexpr int kEb = 4;
   double ex = 0.0;
-  const int q0 = L.roff[ri], q1 = L.roff[ri + 1];
   for (int qb = q0; qb < q1; qb += kEb) {
     float4 e[kEb][3];
     unsigned cc[kEb];
@@ -791,6 +792,9 @@ __device__ __forceinline__ double patch_etdx(const WL& L, const WArgs& A, int ri
     }
   }
   return ex;
+}
+__device__ __forceinline__ double patch_etdx(const WL& L, const WArgs& A, int ri, int par, int N) {
+  return edges_etdx(L, A, L.roff[ri], L.roff[ri + 1], par, N);
 }
 
 __device__ __forceinline__ unsigned wslot(int gp, int t0, int N, int fmin) {
@@ -942,20 +946,36 @@ __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, do
       }
     }
     __syncthreads();
-    // pass 2: thread per patch: C, u, E at a / b in edge order; Schur terms (:554-558)
-    for (int ri = pa + tid; ri < pb; ri += kWT) {
-      double C = 0.0, U = 0.0, Ea[6] = {0, 0, 0, 0, 0, 0}, Eb[6] = {0, 0, 0, 0, 0, 0};
-      for (int q = L.roff[ri]; q < L.roff[ri + 1]; q++) {
-        const double* ps = pe + 14 * (size_t)(q - q0);
-        C += ps[0];
-        U += ps[1];
-        if (MODE != 0) {
+    // pass 2a: thread per (patch, component): C, u, E at a / b summed over the
+    // patch's edges in edge order, 4 edges' reads in flight (a thread per
+    // patch walked ~18 edges one LDS round trip at a time at DPVO sizes,
+    // on one partly filled wave); absent terms add +0.0: the sums are the
+    // per-patch loop's
+    constexpr int NC = (MODE == 2) ? 14 : (MODE == 1 ? 8 : 2);
+    double* psum = pe + 14 * (size_t)kChunk;  // [patch of the chunk][14]
+    for (int t = tid; t < (pb - pa) * NC; t += kWT) {
+      const int rr = t / NC, c = t - rr * NC;
+      const int qa = L.roff[pa + rr], qz = L.roff[pa + rr + 1];
+      double sum = 0.0;
+      for (int qb = qa; qb < qz; qb += 4) {
+        double v[4];
 #pragma unroll
-          for (int k = 0; k < 6; k++) {
-            Ea[k] += ps[2 + k];
-            if (MODE == 2) Eb[k] += ps[8 + k];
-          }
-        }
+        for (int u = 0; u < 4; u++) v[u] = pe[14 * (size_t)(min(qb + u, qz - 1) - q0) + c];
+#pragma unroll
+        for (int u = 0; u < 4; u++) sum += (qb + u < qz) ? v[u] : 0.0;
+      }
+      psum[14 * rr + c] = sum;
+    }
+    __syncthreads();
+    // pass 2b: thread per patch: Q and the Schur terms (:554-558)
+    for (int ri = pa + tid; ri < pb; ri += kWT) {
+      const double* ps = psum + 14 * (size_t)(ri - pa);
+      const double C = ps[0], U = ps[1];
+      double Ea[6], Eb[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) {
+        Ea[k] = (MODE != 0) ? ps[2 + k] : 0.0;
+        Eb[k] = (MODE == 2) ? ps[8 + k] : 0.0;
       }
       const double Q = 1.0 / (C + lam);  // (:519)
       L.qu[ri] = make_double2(Q, U);
@@ -1143,7 +1163,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   mark(A, 41);
   int nrel = tot >> 16, nrp = tot & 0xffff;
   // LDS plan: [head | cnt | patch records | edge records | region | tw | ej]
-  const size_t chunk_b = sizeof(double) * 14 * kChunk;
+  const size_t chunk_b = sizeof(double) * 2 * 14 * kChunk;  // edge records + per-patch sums
   const size_t red_b = sizeof(double) * (36 * 128 + 36 * 8);
   const size_t NN = N > 0 ? N : 1;
   const size_t solve_b =
@@ -1202,12 +1222,19 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     rpo[ri] = po;
     for (int t = 0; t < ne; t++) L.rp[q0 + t] = (unsigned short)ri;
     if (ne > kChunk) ctl[cCap] = 1;
-    // writer of the final depth: the diagonal workgroup of the lowest free
-    // pose with share u % Sd; workgroup 0 for patches without a free pose
+    // writer of the final depth: the diagonal workgroup of one of the
+    // patch's free poses (the ((u / Sd) mod popc(m))-th, so that the oldest
+    // window frames, which most patches see, do not own nearly all of them)
+    // with share u % Sd -- that workgroup linearised every edge of the patch;
+    // workgroup 0 for patches without a free pose
     bool own;
     if (NB == 0) own = true;
     else if (m == 0) own = (g == 0);
-    else own = diag && (int)__builtin_ctz(m) == a && (u % A.Sd) == sub;
+    else {
+      unsigned mm = m;
+      for (int t = (u / A.Sd) % __popc(m); t > 0; t--) mm &= mm - 1;
+      own = diag && (int)__builtin_ctz(mm) == a && (u % A.Sd) == sub;
+    }
     L.pkx[ri] = own ? kx : -1;
     return ri;
   };
@@ -1620,17 +1647,71 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       pl[0] = t1[0]; pl[1] = t1[1]; pl[2] = t1[2];
       pl[3] = q1[0]; pl[4] = q1[1]; pl[5] = q1[2]; pl[6] = q1[3];
     }
-    for (int ri = tid; ri < nrel_e; ri += kWT) {
-      if (L.pkx[ri] < 0) continue;
-      const double ex = patch_etdx(L, A, ri, (it - 1) & 1, N);
-      const double2 qu = L.qu[ri];
-      const float dz = (float)(qu.x * (qu.y - ex));
-      const float base = (it == 1) ? L.dbase[ri] : L.dep[ri];
-      float d = base + dz;
-      d = (d > 20.0f) ? 1.0f : d;
-      L.dep[ri] = (float)fmax((double)d, 1e-4);
+    mark(A, 48);  // final-apply sub-phases (instrumentation): poses retracted
+    if (A.marks && g == 0 && tid == 0) {
+      A.marks[52] = nrp;
+      A.marks[53] = (L.ej ? 2 : 1);  // E entries in LDS, else in the HBM buffer
+    }
+    mark(A, 49);
+    {
+      // the depths this workgroup writes (owned patches); with the E entries
+      // in HBM, kTP threads per patch: each sums E^T dX over a contiguous
+      // part of the patch's edges
+      // (patch_etdx's per-edge order inside the part), the parts are added in
+      // part order -- one HBM round trip of E entries instead of one per 4
+      // edges of a ~18-edge patch on a single thread
+      constexpr int kTP = 8;
+      // region: olist [nrel + 1] (owned flags -> prefix), oidx [nrel], opart [owned][kTP]
+      int* olist = reinterpret_cast<int*>(L.region);
+      double* opart = reinterpret_cast<double*>(L.region + al16(sizeof(int) * (2 * (size_t)nrel_e + 1)));
+      if (L.ej ||
+          al16(sizeof(int) * (2 * (size_t)nrel_e + 1)) + sizeof(double) * kTP * (size_t)nrel_e > region_b) {
+        // E entries in LDS (short patches, cfg2-like windows), or more relevant
+        // patches than the region holds parts for: one thread per patch
+        for (int ri = tid; ri < nrel_e; ri += kWT) {
+          if (L.pkx[ri] < 0) continue;
+          const double ex = patch_etdx(L, A, ri, (it - 1) & 1, N);
+          const double2 qu = L.qu[ri];
+          const float dz = (float)(qu.x * (qu.y - ex));
+          const float base = (it == 1) ? L.dbase[ri] : L.dep[ri];
+          float d = base + dz;
+          d = (d > 20.0f) ? 1.0f : d;
+          L.dep[ri] = (float)fmax((double)d, 1e-4);
+        }
+        olist = nullptr;
+      }
+      if (olist) {
+      for (int ri = tid; ri < nrel_e; ri += kWT) olist[ri] = L.pkx[ri] >= 0 ? 1 : 0;
+      __syncthreads();
+      const int nown = fscan(olist, nrel_e, ctl + cScan);  // olist[ri] = owned patches before ri
+      // compact: owned patch k -> relevant index (stored after the prefix array)
+      int* oidx = olist + nrel_e + 1;
+      for (int ri = tid; ri < nrel_e; ri += kWT)
+        if (L.pkx[ri] >= 0) oidx[olist[ri]] = ri;
+      __syncthreads();
+      for (int t = tid; t < nown * kTP; t += kWT) {
+        const int k = t / kTP, part = t % kTP, ri = oidx[k];
+        const int qa = L.roff[ri], qz = L.roff[ri + 1], len = (qz - qa + kTP - 1) / kTP;
+        const int q0 = min(qa + part * len, qz), q1 = min(q0 + len, qz);
+        opart[t] = edges_etdx(L, A, q0, q1, (it - 1) & 1, N);
+      }
+      __syncthreads();
+      for (int k = tid; k < nown; k += kWT) {
+        const int ri = oidx[k];
+        double ex = 0.0;
+#pragma unroll
+        for (int part = 0; part < kTP; part++) ex += opart[k * kTP + part];
+        const double2 qu = L.qu[ri];
+        const float dz = (float)(qu.x * (qu.y - ex));
+        const float base = (it == 1) ? L.dbase[ri] : L.dep[ri];
+        float d = base + dz;
+        d = (d > 20.0f) ? 1.0f : d;
+        L.dep[ri] = (float)fmax((double)d, 1e-4);
+      }
+      }
     }
     __syncthreads();
+    mark(A, 50);  // depths updated
     for (int k = tid; k < nrel_e * PP; k += kWT) {
       const int ri = k / PP, c = k % PP;
       const int kx = L.pkx[ri];

@@ -65,6 +65,13 @@ for k, v in acc.items():
     v = sorted(v)
     print(f"{k:34s} median {v[len(v) // 2]:8.2f} us")
 
+# final apply of workgroup 0: poses retracted, E entries staged, depths updated, end
+if m[48] and m[50] and m[63] > m[50]:
+    mf = 2 + 8 * (iters - 1) + 3
+    print(f"final apply wg0: poses {(m[48] - m[mf]) * 0.01:.2f} us, depths "
+          f"{(m[50] - m[49]) * 0.01:.2f} us, write-back + status {(m[63] - m[50]) * 0.01:.2f} us"
+          f" (relevant edges {m[52]}, E entries {'in HBM' if m[53] & 1 else 'in LDS'})")
+
 # dense kernel (DPVO_BA_DENSE=1): workgroup 0's pass 0 of iteration 0
 if m[55] and m[58]:
     print(f"dense wg0 pass0: (1) linearise {(m[56] - m[55]) * 0.01:.2f} us, (2) slots "
