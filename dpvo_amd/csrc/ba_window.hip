@@ -952,8 +952,11 @@ __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, do
     // on one partly filled wave); absent terms add +0.0: the sums are the
     // per-patch loop's
     constexpr int NC = (MODE == 2) ? 14 : (MODE == 1 ? 8 : 2);
+    // (only for patches with many edges: at ~2 edges per patch, cfg2, the
+    // per-patch loop below reads them directly and saves the barrier)
+    const bool wide = (q1 - q0) >= 4 * (pb - pa);
     double* psum = pe + 14 * (size_t)kChunk;  // [patch of the chunk][14]
-    for (int t = tid; t < (pb - pa) * NC; t += kWT) {
+    for (int t = tid; wide && t < (pb - pa) * NC; t += kWT) {
       const int rr = t / NC, c = t - rr * NC;
       const int qa = L.roff[pa + rr], qz = L.roff[pa + rr + 1];
       double sum = 0.0;
@@ -966,16 +969,36 @@ __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, do
       }
       psum[14 * rr + c] = sum;
     }
-    __syncthreads();
+    if (wide) __syncthreads();
     // pass 2b: thread per patch: Q and the Schur terms (:554-558)
     for (int ri = pa + tid; ri < pb; ri += kWT) {
-      const double* ps = psum + 14 * (size_t)(ri - pa);
-      const double C = ps[0], U = ps[1];
-      double Ea[6], Eb[6];
+      double C, U, Ea[6], Eb[6];
+      if (wide) {
+        const double* ps = psum + 14 * (size_t)(ri - pa);
+        C = ps[0];
+        U = ps[1];
 #pragma unroll
-      for (int k = 0; k < 6; k++) {
-        Ea[k] = (MODE != 0) ? ps[2 + k] : 0.0;
-        Eb[k] = (MODE == 2) ? ps[8 + k] : 0.0;
+        for (int k = 0; k < 6; k++) {
+          Ea[k] = (MODE != 0) ? ps[2 + k] : 0.0;
+          Eb[k] = (MODE == 2) ? ps[8 + k] : 0.0;
+        }
+      } else {  // the patch's edges in order (the same sums)
+        C = 0.0;
+        U = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; k++) Ea[k] = Eb[k] = 0.0;
+        for (int q = L.roff[ri]; q < L.roff[ri + 1]; q++) {
+          const double* ps = pe + 14 * (size_t)(q - q0);
+          C += ps[0];
+          U += ps[1];
+          if (MODE != 0) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+              Ea[k] += ps[2 + k];
+              if (MODE == 2) Eb[k] += ps[8 + k];
+            }
+          }
+        }
       }
       const double Q = 1.0 / (C + lam);  // (:519)
       L.qu[ri] = make_double2(Q, U);
