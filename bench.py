@@ -37,7 +37,7 @@ sys.path.insert(0, REPO)
 METRIC = "update-iterations/sec (altcorr+fastba) on 96-patch/2048-edge graph, 1→8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                            "profiles", "r03_corr_traffic.json")
+                            "profiles", "r04_corr_traffic.json")
 
 
 def pmc_traffic(config):
@@ -456,6 +456,7 @@ def main():
                               "to the reference's fp64 run (tests/test_cpu_baseline.py)"}
 
     if rank == 0:
+        traffic = pmc_traffic(args.config) if args.features == "f32" else None
         out = {
             "metric": METRIC,
             "value": value,
@@ -494,7 +495,11 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": pmc_traffic(args.config) if args.features == "f32" else None,
+                "traffic": traffic,
+                # counter (real DRAM) rate of the same launch: PMC bytes / the
+                # live kernel time; below `achieved` because edges sharing a
+                # target frame re-read overlapping boxes from L2 / MALL
+                "traffic_gbs": (traffic / (corr_ms * 1e-3) / 1e9) if traffic else None,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "kernel_ms": corr_ms,
                 "per_level": per_level,
