@@ -72,12 +72,21 @@ constexpr int kStChol = 1, kStClamp = 2, kStTimeout = 16, kStCap = 32;
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
+// plan meta (ints): [0] nuniq, [1] fmin, [2] status, [3] shards that wrote
+// block-work partials; [16, 28) int64 phase stamps; [kMetaWork + s * kWMaxNB
+// + lblk(a, b)] edges of the patches whose free poses hold a and b, from shard
+// s (ba_window_kernel gives each lower block workgroups in proportion)
+constexpr int kWMaxNB = kWMaxN * (kWMaxN + 1) / 2;
+constexpr int kPlanShardMax = 16;
+constexpr int kMetaWork = 64;
+constexpr size_t kMetaBytes = sizeof(int) * (kMetaWork + (size_t)kPlanShardMax * kWMaxNB);
+
 struct Plan {          // written by ba_plan_kernel, read by ba_window_kernel
   int* epos;           // [E] edge index at sorted position p (grouped by patch)
   int* poff;           // [E + 1] first position of patch u
   unsigned* pmask;     // [E] free-pose bitmask of patch u
   int* pkk;            // [E] patch id (kk) of patch u
-  int* meta;           // [8] nuniq, fmin, status
+  int* meta;           // [kMetaBytes / 4]: nuniq, fmin, status, shards, stamps, block work
   int* status;         // the workspace status word, reset here
   int* sink;           // caller's sticky status word or null
   const int* t0d;      // device t0 (graph-replayed updates: t0 moves per frame) or null
@@ -94,6 +103,7 @@ struct WArgs {
   const int64_t* jj;
   const int64_t* kk;
   int E, P, num_poses, num_patches, t0, N, iters, NB, Sd, So, G;
+  int dw;  // diagonal-block work weight in quarters for the plan-driven split (0: diagonals keep Sd)
   Plan plan;
   double* part;      // [2][G][kPartPad] published partial blocks, by iteration parity (flag modes)
   v4u* gran;         // [2][G][kGranPad] the same as 16-B granules (default mode);
@@ -128,22 +138,6 @@ __device__ __forceinline__ void mark(const WArgs& A, int slot) {
   if (A.marks && blockIdx.x == 0 && threadIdx.x == 0) A.marks[slot] = (int64_t)wall_clock64();
 }
 
-// workgroup g -> (block a, b; share sub of S shares).  Diagonal blocks first.
-__device__ __forceinline__ void wg_block(const WArgs& A, int g, int& a, int& b, int& sub, int& S) {
-  const int nd = A.N * A.Sd;
-  if (g < nd) {
-    a = b = g / A.Sd;
-    sub = g % A.Sd;
-    S = A.Sd;
-  } else {
-    const int o = (g - nd) / A.So;  // o-th strictly lower block, row-major
-    sub = (g - nd) % A.So;
-    S = A.So;
-    a = 1;  // (a, b), a > b, at o = a(a-1)/2 + b
-    while ((a + 1) * a / 2 <= o) a++;
-    b = o - a * (a - 1) / 2;
-  }
-}
 
 // ===========================================================================
 // plan: group edges by patch (one workgroup, 512 threads)
@@ -249,6 +243,29 @@ __device__ __forceinline__ void plan_edges_pass(const int64_t* __restrict__ ii,
   __syncthreads();
 }
 
+// Block work of a set of patches (plan side): wl[lblk(a, b)] += edges of
+// every patch whose free-pose mask holds a and b; patch(t) -> (count, mask)
+// for t < n.  wl: kWMaxNB ints of LDS, zeroed by the caller before a barrier.
+template <typename F>
+__device__ __forceinline__ void plan_block_work(int n, F patch, int* wl) {
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    int c;
+    unsigned m;
+    patch(t, c, m);
+    if (c <= 0) continue;
+    for (unsigned ma = m; ma; ma &= ma - 1) {
+      const int x = __builtin_ctz(ma);
+      for (unsigned mb = m & ((2u << x) - 1u); mb; mb &= mb - 1)  // y <= x
+        atomicAdd(&wl[lblk(x, __builtin_ctz(mb))], c);
+    }
+  }
+}
+__device__ __forceinline__ void plan_store_work(const Plan& plan, const int* wl, int s, int N) {
+  const int nb = N * (N + 1) / 2;
+  for (int t = threadIdx.x; t < nb; t += blockDim.x)
+    plan.meta[kMetaWork + s * kWMaxNB + t] = wl[t];
+}
+
 __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
                                            const int64_t* __restrict__ jj,
                                            const int64_t* __restrict__ kk, int E, int num_patches,
@@ -326,6 +343,7 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
       plan.meta[0] = nuniq;
       plan.meta[1] = ctl[2];
       plan.meta[2] = ctl[3];
+      plan.meta[3] = 0;  // no block-work partials: the iteration kernel splits blocks evenly
       if (ctl[3] && plan.sink) atomicOr(plan.sink, ctl[3]);
       *plan.status = 0;  // this call's status word (ORed by the iteration kernel)
     }
@@ -473,6 +491,7 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
     plan.meta[0] = nuniq;
     plan.meta[1] = ctl[2];
     plan.meta[2] = ctl[3];
+    plan.meta[3] = 0;
     if (ctl[3] && plan.sink) atomicOr(plan.sink, ctl[3]);
     *plan.status = 0;  // this call's status word (ORed by the iteration kernel)
   }
@@ -489,7 +508,6 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
 // The shards write disjoint ranges of epos / poff / pkk / pmask: no exchange
 // between workgroups.  Falls back to plan_block in shard 0 when the kk range
 // or the LDS does not fit.
-constexpr int kPlanShardMax = 16;
 __host__ __device__ constexpr int plan_shards(int E) {
   return E <= 512 ? 1 : ((E + 511) / 512 < kPlanShardMax ? (E + 511) / 512 : kPlanShardMax);
 }
@@ -523,7 +541,7 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
   const int kmin = ctl[0], R = ctl[1] - kmin + 1;
   const int nlmax = (R + S - 1) / S;
   const bool fits = E > 0 && R <= kHistMax && E < (1 << 14) &&
-                    256 + 4 * (size_t)cap + 4 * (size_t)R + 4 * (size_t)nlmax <= lds_bytes;
+                    256 + 4 * (size_t)cap + 4 * (size_t)R + 4 * (size_t)nlmax + 4 * kWMaxNB <= lds_bytes;
   if (!fits) {  // shard-uniform (every shard saw the same edges)
     if (s == 0) {
       __syncthreads();  // ctl is re-initialised by plan_block
@@ -533,8 +551,10 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
   }
   const int lo = (int)((long long)R * s / S), hi = (int)((long long)R * (s + 1) / S), nl = hi - lo;
   unsigned* pm = reinterpret_cast<unsigned*>(hf + R);
+  int* wl = reinterpret_cast<int*>(pm + nl);  // [kWMaxNB] block work of this shard's patches
   for (int v = tid; v < R; v += T) hf[v] = 0;
   for (int v = tid; v < nl; v += T) pm[v] = 0u;
+  for (int v = tid; v < kWMaxNB; v += T) wl[v] = 0;
   if (tid == 0) {
     ctl[4] = 0;
     ctl[5] = 0;
@@ -589,6 +609,12 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
   }
   __syncthreads();
   stamp(4);
+  // block work of the local patches (bucket v: edges end(v) - end(v - 1))
+  plan_block_work(nl, [&](int v, int& c, unsigned& m) {
+    const int hv = hist[v];
+    c = (hv >> 14) - (v == 0 ? 0 : (hist[v - 1] >> 14));
+    m = pm[hv & 0x3fff];
+  }, wl);
 #pragma unroll
   for (int r = 0; r < kPlanPer; r++) {
     const int e = tid + r * T;
@@ -605,11 +631,14 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
       plan.pmask[u] = pm[hv & 0x3fff];
     }
   }
+  __syncthreads();  // block work complete (the rank loop above does not touch wl)
+  plan_store_work(plan, wl, s, N);
   if (tid == 0 && s == S - 1) plan.poff[nuniq] = E;
   if (tid == 0 && s == 0) {
     plan.meta[0] = nuniq;
     plan.meta[1] = ctl[2];
     plan.meta[2] = ctl[3];
+    plan.meta[3] = S;
     if (ctl[3] && plan.sink) atomicOr(plan.sink, ctl[3]);
     *plan.status = 0;
   }
@@ -1095,9 +1124,6 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, g = blockIdx.x;
   const int N = A.N, P = A.P, PP = P * P, NB = A.NB;
-  int a = 0, b = 0, sub = 0, S = 1;
-  if (NB > 0) wg_block(A, g, a, b, sub, S);
-  const bool diag = (a == b);
   const float fx = A.intrinsics[0], fy = A.intrinsics[1], cx = A.intrinsics[2],
               cy = A.intrinsics[3];
   const int t0w = A.t0d ? *A.t0d : A.t0;  // first free pose
@@ -1125,17 +1151,9 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     tri_of(t, ta, tb);
     L.tri[t] = (unsigned short)((ta << 8) | tb);
   }
-  // ---------------- setup: relevant patches of this workgroup ----------------
-  // rel(u): mask holds a and b and u % S == sub; workgroup 0 also takes the
-  // patches without a free pose (their dZ = Q u).  One scan packs
-  // (#patches << 16 | #edges) (E <= 4096 keeps both below 2^16).
-  // Global round trips are the setup's cost (~1 us each on a cold L2): the
-  // plan meta and the first kB * 256 patches' plan entries are loaded in ONE
-  // batch (speculatively, indices clamped to the E-sized arrays), then the
-  // patch values, the edge ids and the pose table in a second, then the
-  // per-edge inputs in a third.
+  // The first batch of plan entries (below) does not depend on the block: it
+  // is issued before the block-work loads so both share one round trip.
   constexpr int kB = 8;
-  const unsigned need = (NB > 0) ? ((1u << a) | (1u << b)) : 0u;
   unsigned m0[kB];
   int pa0[kB], pb0[kB], kx0[kB];
 #pragma unroll
@@ -1147,6 +1165,99 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     kx0[r] = A.plan.pkk[u];
   }
   const int nuniq = A.plan.meta[0], fmin = A.plan.meta[1];
+  // ---------------- workgroups -> lower blocks ----------------
+  // Blocks in the order diagonal (j < N: (j, j)) then strictly lower
+  // row-major (j = N + a (a - 1) / 2 + b); block j gets workgroups
+  // [bstart[j], bstart[j + 1]).  Diagonal blocks: the host's Sd each.  Lower
+  // blocks: one each, the rest of the grid in proportion to their work from
+  // the plan (edges of the patches whose free poses hold both poses: the
+  // block's re-linearisation count), so that the blocks of the oldest window
+  // frames, which most patches see, get more shares (E = 3940: kernel 63.8 ->
+  // 53.6 us).  Without partials (small plans) the split is the host's So.
+  int* bstart = reinterpret_cast<int*>(lds + off);  // [NB + 1]
+  off = al16(off + sizeof(int) * (kWMaxNB + 1));
+  const int gx = A.G - N * A.Sd - (NB - N);  // shares beyond Sd per diagonal, one per lower block
+  if (gx <= 0) {  // nothing to distribute (cfg2's grid): the host's split, no plan loads
+    if (tid <= NB) bstart[tid] = tid <= N ? tid * A.Sd : N * A.Sd + (tid - N) * A.So;
+    __syncthreads();
+  } else {
+    const int nsh = A.plan.meta[3];
+    int wj = 0;
+    if (tid < NB) {
+      int ja = tid, jb = tid;  // block of order index tid
+      if (tid >= N) {
+        const int o = tid - N;
+        ja = 1;
+        while ((ja + 1) * ja / 2 <= o) ja++;
+        jb = o - ja * (ja - 1) / 2;
+      }
+      int w16[kPlanShardMax];
+#pragma unroll
+      for (int q = 0; q < kPlanShardMax; q++) w16[q] = A.plan.meta[kMetaWork + q * kWMaxNB + lblk(ja, jb)];
+#pragma unroll
+      for (int q = 0; q < kPlanShardMax; q++) wj += q < nsh ? w16[q] : 0;
+      if (A.dw > 0) wj *= (tid < N) ? A.dw : 4;
+      bstart[tid] = wj;
+    }
+    __syncthreads();
+    mark(A, 44);
+    const int wtot = fscan(bstart, NB, ctl + cScan);  // bstart[j] = work of blocks before j
+    mark(A, 45);
+    int st = 0;
+    if (tid <= NB) {
+      // diagonal blocks keep the host's Sd shares (their per-edge work -- B
+      // terms of every edge at the pose, the y entries -- is not what the
+      // edge count measures); the strictly lower blocks share the rest, one
+      // each plus the remainder in proportion to their work
+      const int cumd = N < NB ? bstart[N] : wtot;  // work of the diagonal blocks
+      const int woff = wtot - cumd;
+      if (A.dw > 0 && nsh > 0 && wtot > 0) {  // every block: one share + its weighted part of the rest
+        const long long cum = tid < NB ? bstart[tid] : wtot;
+        st = tid + (int)((long long)(A.G - NB) * cum / wtot);
+      } else if (tid <= N) {
+        st = tid * A.Sd;
+      } else if (nsh > 0 && woff > 0) {
+        const long long cum = (tid < NB ? bstart[tid] : wtot) - cumd;
+        st = N * A.Sd + (tid - N) + (int)((long long)gx * cum / woff);
+      } else {  // no plan partials: the host's split
+        st = N * A.Sd + (tid - N) * A.So;
+      }
+    }
+    __syncthreads();  // every prefix read before any is overwritten
+    if (tid <= NB) bstart[tid] = st;
+    __syncthreads();
+    mark(A, 46);
+  }
+  int a = 0, b = 0, sub = 0, S = 1;
+  if (NB > 0) {
+    int lo = 0, hi = NB - 1;  // last j with bstart[j] <= g
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (bstart[mid] <= g) lo = mid; else hi = mid - 1;
+    }
+    sub = g - bstart[lo];
+    S = bstart[lo + 1] - bstart[lo];
+    if (lo < N) {
+      a = b = lo;
+    } else {
+      const int o = lo - N;
+      a = 1;
+      while ((a + 1) * a / 2 <= o) a++;
+      b = o - a * (a - 1) / 2;
+    }
+  }
+  const bool diag = (a == b);
+  auto diag_shares = [&](int p) { return bstart[p + 1] - bstart[p]; };
+  // ---------------- setup: relevant patches of this workgroup ----------------
+  // rel(u): mask holds a and b and u % S == sub; workgroup 0 also takes the
+  // patches without a free pose (their dZ = Q u).  One scan packs
+  // (#patches << 16 | #edges) (E <= 4096 keeps both below 2^16).
+  // Global round trips are the setup's cost (~1 us each on a cold L2): the
+  // plan meta and the first kB * 256 patches' plan entries are loaded in ONE
+  // batch (speculatively, indices clamped to the E-sized arrays), then the
+  // patch values, the edge ids and the pose table in a second, then the
+  // per-edge inputs in a third.
+  const unsigned need = (NB > 0) ? ((1u << a) | (1u << b)) : 0u;
   if (tid == 0) {
     ctl[cFail] = 0;
     ctl[cFailAny] = 0;
@@ -1246,17 +1357,20 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     for (int t = 0; t < ne; t++) L.rp[q0 + t] = (unsigned short)ri;
     if (ne > kChunk) ctl[cCap] = 1;
     // writer of the final depth: the diagonal workgroup of one of the
-    // patch's free poses (the ((u / Sd) mod popc(m))-th, so that the oldest
+    // patch's free poses (the ((u / 4) mod popc(m))-th, so that the oldest
     // window frames, which most patches see, do not own nearly all of them)
-    // with share u % Sd -- that workgroup linearised every edge of the patch;
+    // with share u % (its shares) -- that workgroup linearised every edge of
+    // the patch;
     // workgroup 0 for patches without a free pose
     bool own;
     if (NB == 0) own = true;
     else if (m == 0) own = (g == 0);
     else {
       unsigned mm = m;
-      for (int t = (u / A.Sd) % __popc(m); t > 0; t--) mm &= mm - 1;
-      own = diag && (int)__builtin_ctz(mm) == a && (u % A.Sd) == sub;
+      // (the owner's diagonal block is split in diag_shares(p) shares, p its pose)
+      for (int t = (u >> 2) % __popc(m); t > 0; t--) mm &= mm - 1;
+      const int po = __builtin_ctz(mm);
+      own = diag && po == a && (u % diag_shares(po)) == sub;
     }
     L.pkx[ri] = own ? kx : -1;
     return ri;
@@ -1473,7 +1587,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     // hash check out, so the gather overlaps the wait for the slowest
     // workgroup and the tail after it is one load round trip.
     {
-      const int ndg = NNb * A.Sd;  // diagonal slots hold 27 granules, the others 36
+      const int ndg = bstart[NNb];  // diagonal blocks' workgroups first: 27 granules, the others 36
       const int T = ndg * 27 + (A.G - ndg) * 36;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           gbuf, 0, (int)(16 * kGranPad * (size_t)A.G), kBufDword3);
@@ -1617,19 +1731,18 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
         const int x = k / 6, z = k % 6;
         const int xx = x >= z ? x : z, zz = x >= z ? z : x;
         const int li = xx * (xx + 1) / 2 + zz;
-        for (int sb = 0; sb < A.Sd; sb++) s += pc[(ba_ * A.Sd + sb) * kPartPad + li];
+        for (int sb = bstart[ba_]; sb < bstart[ba_ + 1]; sb++) s += pc[sb * kPartPad + li];
         if (x == z) s += 1e-4 * s + 1.0;  // S += I (1e-4 S + 1) (ba_cuda.cu:560)
       } else {
         const int o = ba_ * (ba_ - 1) / 2 + bb_;
-        const int g0 = NNb * A.Sd + o * A.So;
-        for (int sb = 0; sb < A.So; sb++) s += pc[(g0 + sb) * kPartPad + k];
+        for (int sb = bstart[NNb + o]; sb < bstart[NNb + o + 1]; sb++) s += pc[sb * kPartPad + k];
       }
       Sd[t] = s;
     }
     for (int t = tid; t < 6 * N; t += kWT) {
       const int i = t / 6, x = t % 6;
       double s = 0.0;
-      for (int sb = 0; sb < A.Sd; sb++) s += pc[(i * A.Sd + sb) * kPartPad + 21 + x];
+      for (int sb = bstart[i]; sb < bstart[i + 1]; sb++) s += pc[sb * kPartPad + 21 + x];
       yd[t] = s;
     }
     __syncthreads();
@@ -2434,6 +2547,18 @@ static bool use_dense(int E) {
   if (ov && (ov[0] == '0' || ov[0] == '1')) return ov[0] == '1';
   return false;
 }
+// plan-driven split (grids with more than Sd shares per diagonal and one per
+// lower block to give out): weight of a diagonal block's edge count against a
+// lower block's, in quarters; 0 keeps Sd per diagonal.  DPVO_BA_DIAGW overrides.
+static int diag_weight() {
+  static const int w = [] {
+    const char* ov = getenv("DPVO_BA_DIAGW");
+    int v = 0;
+    if (ov && sscanf(ov, "%d", &v) == 1 && v >= 0 && v <= 64) return v;
+    return 0;
+  }();
+  return w;
+}
 static WGrid window_grid(int E, int N) {
   WGrid w;
   w.NB = N * (N + 1) / 2;
@@ -2519,7 +2644,7 @@ size_t ba_window_scratch_bytes(int E, int N) {
   const WGrid w = window_grid(E, N);
   return al256w(sizeof(int) * (size_t)E) + al256w(sizeof(int) * (size_t)(E + 1)) +
          al256w(sizeof(unsigned) * (size_t)E) + al256w(sizeof(int) * (size_t)E) +
-         al256w(sizeof(int) * 8) + al256w(sizeof(double) * 2 * kPartPad * (size_t)w.G) +
+         al256w(kMetaBytes) + al256w(sizeof(double) * 2 * kPartPad * (size_t)w.G) +
          al256w((size_t)16 * gran_count(w)) + al256w(sizeof(float) * 24 * (size_t)E);
 }
 
@@ -2746,7 +2871,7 @@ int ba_window_run(float* poses, float* patches, const float* intrinsics, const f
   a.plan = plan_view(scratch, E, status);
   char* s = scratch + al256w(sizeof(int) * (size_t)E) + al256w(sizeof(int) * (size_t)(E + 1)) +
             al256w(sizeof(unsigned) * (size_t)E) + al256w(sizeof(int) * (size_t)E) +
-            al256w(sizeof(int) * 8);
+            al256w(kMetaBytes);
   a.part = (double*)s;
   s += al256w(sizeof(double) * 2 * kPartPad * (size_t)w.G);
   a.gran = (v4u*)s;
@@ -2774,6 +2899,7 @@ int ba_window_run(float* poses, float* patches, const float* intrinsics, const f
   a.Sd = w.Sd;
   a.So = w.So;
   a.G = w.G;
+  a.dw = diag_weight();
   a.status = status;
   a.sink = a.plan.sink;
   a.marks = marks;

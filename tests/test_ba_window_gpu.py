@@ -257,6 +257,25 @@ def _host_grouping(ii, jj, kk, t0, t1):
     return order.astype(np.int32), poff.astype(np.int32), pmask, uk.astype(np.int32)
 
 
+def _check_block_work(meta, ref, N):
+    """The sharded plan's block work (meta[64 + s * 136 + lblk(a, b)], shards
+    s < meta[3]): edges of the patches whose free-pose mask holds a and b."""
+    nsh = int(meta[3])
+    if nsh == 0:  # single-workgroup plan: no partials (the kernel splits evenly)
+        return
+    got = meta[64:64 + 16 * 136].reshape(16, 136)[:nsh].sum(0)
+    want = np.zeros(136, np.int64)
+    poff, pmask = ref[1], ref[2]
+    for u in range(pmask.size):
+        c, m = int(poff[u + 1] - poff[u]), int(pmask[u])
+        bits = [x for x in range(N) if (m >> x) & 1]
+        for x in bits:
+            for y in bits:
+                if y <= x:
+                    want[x * (x + 1) // 2 + y] += c
+    np.testing.assert_array_equal(got[:N * (N + 1) // 2], want[:N * (N + 1) // 2])
+
+
 def _plan_arrays(cb, ws, E, t0, t1):
     off = cb.plan_offsets(E, t0, t1)
     b = ws.cpu().numpy()
@@ -264,7 +283,7 @@ def _plan_arrays(cb, ws, E, t0, t1):
     def arr(k, n, dt):
         return np.frombuffer(b[off[k]:off[k] + 4 * n].tobytes(), dt)
 
-    meta = arr(4, 8, np.int32)
+    meta = arr(4, 64 + 16 * 136, np.int32)  # kMetaWork + kPlanShardMax * kWMaxNB
     nuniq = int(meta[0])
     return (arr(0, E, np.int32), arr(1, nuniq + 1, np.int32), arr(2, nuniq, np.uint32),
             arr(3, nuniq, np.int32), nuniq, meta)
@@ -305,6 +324,7 @@ def test_plan_grouping_matches_host(cb, gpu, E, nk, M, seed):
         epos, poff, pmask, pkk, nuniq, meta = _plan_arrays(cb, ws, E, t0, t1)
         assert nuniq == ref[3].size
         assert int(meta[1]) == fmin and int(meta[2]) == 0  # smallest fixed pose, no clamp
+        _check_block_work(meta, ref, t1 - t0)
         np.testing.assert_array_equal(pkk, ref[3])
         np.testing.assert_array_equal(poff, ref[1])
         np.testing.assert_array_equal(epos, ref[0])
