@@ -103,7 +103,6 @@ struct WArgs {
   const int64_t* jj;
   const int64_t* kk;
   int E, P, num_poses, num_patches, t0, N, iters, NB, Sd, So, G;
-  int dw;  // diagonal-block work weight in quarters for the plan-driven split (0: diagonals keep Sd)
   Plan plan;
   double* part;      // [2][G][kPartPad] published partial blocks, by iteration parity (flag modes)
   v4u* gran;         // [2][G][kGranPad] the same as 16-B granules (default mode);
@@ -1167,84 +1166,89 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   const int nuniq = A.plan.meta[0], fmin = A.plan.meta[1];
   // ---------------- workgroups -> lower blocks ----------------
   // Blocks in the order diagonal (j < N: (j, j)) then strictly lower
-  // row-major (j = N + a (a - 1) / 2 + b); block j gets workgroups
+  // row-major (j = N + o, o = a (a - 1) / 2 + b); block j gets workgroups
   // [bstart[j], bstart[j + 1]).  Diagonal blocks: the host's Sd each.  Lower
-  // blocks: one each, the rest of the grid in proportion to their work from
-  // the plan (edges of the patches whose free poses hold both poses: the
-  // block's re-linearisation count), so that the blocks of the oldest window
-  // frames, which most patches see, get more shares (E = 3940: kernel 63.8 ->
-  // 53.6 us).  Without partials (small plans) the split is the host's So.
+  // blocks: when the host grid has shares to give out (So > 1), one each plus
+  // the rest in proportion to their work from the plan (edges of the patches
+  // whose free poses hold both poses: the block's re-linearisation count), so
+  // that the blocks of the oldest window frames, which most patches see, get
+  // more shares (E = 3940: kernel 63.8 -> 54.0 us); otherwise So each.
+  // Every wave computes the split in registers (lane l: lower blocks 2l and
+  // 2l + 1, one DPP scan, a ballot finds this workgroup's block): no LDS
+  // round trip and no barrier; wave 0 leaves bstart in LDS for the gather,
+  // ordered before its readers by the setup's barriers.
   int* bstart = reinterpret_cast<int*>(lds + off);  // [NB + 1]
   off = al16(off + sizeof(int) * (kWMaxNB + 1));
-  const int gx = A.G - N * A.Sd - (NB - N);  // shares beyond Sd per diagonal, one per lower block
-  if (gx <= 0) {  // nothing to distribute (cfg2's grid): the host's split, no plan loads
-    if (tid <= NB) bstart[tid] = tid <= N ? tid * A.Sd : N * A.Sd + (tid - N) * A.So;
-    __syncthreads();
-  } else {
-    const int nsh = A.plan.meta[3];
-    int wj = 0;
-    if (tid < NB) {
-      int ja = tid, jb = tid;  // block of order index tid
-      if (tid >= N) {
-        const int o = tid - N;
-        ja = 1;
-        while ((ja + 1) * ja / 2 <= o) ja++;
-        jb = o - ja * (ja - 1) / 2;
-      }
-      int w16[kPlanShardMax];
-#pragma unroll
-      for (int q = 0; q < kPlanShardMax; q++) w16[q] = A.plan.meta[kMetaWork + q * kWMaxNB + lblk(ja, jb)];
-#pragma unroll
-      for (int q = 0; q < kPlanShardMax; q++) wj += q < nsh ? w16[q] : 0;
-      if (A.dw > 0) wj *= (tid < N) ? A.dw : 4;
-      bstart[tid] = wj;
-    }
-    __syncthreads();
-    mark(A, 44);
-    const int wtot = fscan(bstart, NB, ctl + cScan);  // bstart[j] = work of blocks before j
-    mark(A, 45);
-    int st = 0;
-    if (tid <= NB) {
-      // diagonal blocks keep the host's Sd shares (their per-edge work -- B
-      // terms of every edge at the pose, the y entries -- is not what the
-      // edge count measures); the strictly lower blocks share the rest, one
-      // each plus the remainder in proportion to their work
-      const int cumd = N < NB ? bstart[N] : wtot;  // work of the diagonal blocks
-      const int woff = wtot - cumd;
-      if (A.dw > 0 && nsh > 0 && wtot > 0) {  // every block: one share + its weighted part of the rest
-        const long long cum = tid < NB ? bstart[tid] : wtot;
-        st = tid + (int)((long long)(A.G - NB) * cum / wtot);
-      } else if (tid <= N) {
-        st = tid * A.Sd;
-      } else if (nsh > 0 && woff > 0) {
-        const long long cum = (tid < NB ? bstart[tid] : wtot) - cumd;
-        st = N * A.Sd + (tid - N) + (int)((long long)gx * cum / woff);
-      } else {  // no plan partials: the host's split
-        st = N * A.Sd + (tid - N) * A.So;
-      }
-    }
-    __syncthreads();  // every prefix read before any is overwritten
-    if (tid <= NB) bstart[tid] = st;
-    __syncthreads();
-    mark(A, 46);
+  const int gd = N * A.Sd, nlow = NB - N;
+  const int gx = A.G - gd - nlow;  // shares beyond Sd per diagonal and one per lower block
+  int blk = 0, sub = 0, S = 1;
+  if (NB > 0 && g < gd) {
+    blk = g / A.Sd;
+    sub = g - blk * A.Sd;
+    S = A.Sd;
   }
-  int a = 0, b = 0, sub = 0, S = 1;
-  if (NB > 0) {
-    int lo = 0, hi = NB - 1;  // last j with bstart[j] <= g
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (bstart[mid] <= g) lo = mid; else hi = mid - 1;
+  if (gx > 0 && nlow > 0) {
+    const int lane = tid & 63;
+    const int nsh = A.plan.meta[3];
+    int w2[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int o = min(2 * lane + h, nlow - 1);  // clamped: loads stay unconditional
+      int ja = 1;
+      while ((ja + 1) * ja / 2 <= o) ja++;
+      const int* src = A.plan.meta + kMetaWork + o + ja;  // lblk(ja, jb) = o + ja
+      int wq[kPlanShardMax];
+#pragma unroll
+      for (int q = 0; q < kPlanShardMax; q++) wq[q] = src[q * kWMaxNB];
+      int w = 0;
+#pragma unroll
+      for (int q = 0; q < kPlanShardMax; q++) w += q < nsh ? wq[q] : 0;
+      w2[h] = (2 * lane + h < nlow) ? w : 0;
     }
-    sub = g - bstart[lo];
-    S = bstart[lo + 1] - bstart[lo];
-    if (lo < N) {
-      a = b = lo;
-    } else {
-      const int o = lo - N;
-      a = 1;
-      while ((a + 1) * a / 2 <= o) a++;
-      b = o - a * (a - 1) / 2;
+    const int incl = wave_incl_sum(w2[0] + w2[1]);
+    const int woff = __builtin_amdgcn_readlane(incl, 63);
+    const bool prop = nsh > 0 && woff > 0;  // else the host's So each
+    auto share0 = [&](int o, int cum) {
+      return gd + (prop ? o + (int)((long long)gx * cum / woff) : o * A.So);
+    };
+    const int ex = incl - w2[0] - w2[1];
+    const int st0 = share0(2 * lane, ex), st1 = share0(2 * lane + 1, ex + w2[0]);
+    if (tid < 64) {
+      if (2 * lane < nlow) bstart[N + 2 * lane] = st0;
+      if (2 * lane + 1 < nlow) bstart[N + 2 * lane + 1] = st1;
     }
+    if (g >= gd) {
+      const unsigned long long b0 = __ballot(2 * lane < nlow && st0 <= g);
+      const unsigned long long b1 = __ballot(2 * lane + 1 < nlow && st1 <= g);
+      const int o = __popcll(b0) + __popcll(b1) - 1;  // st(0) = gd <= g
+      const int s_o = __builtin_amdgcn_readlane((o & 1) ? st1 : st0, o >> 1);
+      const int s_n = (o + 1 >= nlow) ? A.G
+                                      : __builtin_amdgcn_readlane(((o + 1) & 1) ? st1 : st0,
+                                                                  (o + 1) >> 1);
+      blk = N + o;
+      sub = g - s_o;
+      S = s_n - s_o;
+    }
+  } else {
+    if (tid > N && tid < NB) bstart[tid] = gd + (tid - N) * A.So;
+    if (NB > 0 && g >= gd) {
+      const int o = (g - gd) / A.So;
+      blk = N + o;
+      sub = g - gd - o * A.So;
+      S = A.So;
+    }
+  }
+  if (tid <= N) bstart[tid] = tid * A.Sd;
+  if (tid == 0) bstart[NB] = A.G;
+  int a = 0, b = 0;
+  if (NB == 0) {
+  } else if (blk < N) {
+    a = b = blk;
+  } else {
+    const int o = blk - N;
+    a = 1;
+    while ((a + 1) * a / 2 <= o) a++;
+    b = o - a * (a - 1) / 2;
   }
   const bool diag = (a == b);
   auto diag_shares = [&](int p) { return bstart[p + 1] - bstart[p]; };
@@ -2547,18 +2551,6 @@ static bool use_dense(int E) {
   if (ov && (ov[0] == '0' || ov[0] == '1')) return ov[0] == '1';
   return false;
 }
-// plan-driven split (grids with more than Sd shares per diagonal and one per
-// lower block to give out): weight of a diagonal block's edge count against a
-// lower block's, in quarters; 0 keeps Sd per diagonal.  DPVO_BA_DIAGW overrides.
-static int diag_weight() {
-  static const int w = [] {
-    const char* ov = getenv("DPVO_BA_DIAGW");
-    int v = 0;
-    if (ov && sscanf(ov, "%d", &v) == 1 && v >= 0 && v <= 64) return v;
-    return 0;
-  }();
-  return w;
-}
 static WGrid window_grid(int E, int N) {
   WGrid w;
   w.NB = N * (N + 1) / 2;
@@ -2899,7 +2891,6 @@ int ba_window_run(float* poses, float* patches, const float* intrinsics, const f
   a.Sd = w.Sd;
   a.So = w.So;
   a.G = w.G;
-  a.dw = diag_weight();
   a.status = status;
   a.sink = a.plan.sink;
   a.marks = marks;

@@ -43,9 +43,6 @@ for rep in range(40):
         continue
     d = {"call (events)": e0.elapsed_time(e1) * 1e3, "kernel (marks)": (m[63] - m[0]) * 0.01,
          "setup": (m[1] - m[0]) * 0.01,
-         "  setup: block map (loads, scan, split)": (m[46] - m[0]) * 0.01 if m[46] > m[0] else 0.0,
-         "    map: block-work loads": (m[44] - m[0]) * 0.01 if m[44] > m[0] else 0.0,
-         "    map: scan": (m[45] - m[44]) * 0.01 if m[45] > m[44] else 0.0,
          "  setup: plan entries + counts": (m[40] - m[0]) * 0.01,
          "  setup: scan": (m[41] - m[40]) * 0.01,
          "  setup: records": (m[42] - m[41]) * 0.01,
