@@ -73,9 +73,10 @@ constexpr int kStChol = 1, kStClamp = 2, kStTimeout = 16, kStCap = 32;
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // plan meta (ints): [0] nuniq, [1] fmin, [2] status, [3] shards that wrote
-// block-work partials; [16, 28) int64 phase stamps; [kMetaWork + s * kWMaxNB
-// + lblk(a, b)] edges of the patches whose free poses hold a and b, from shard
-// s (ba_window_kernel gives each lower block workgroups in proportion)
+// block-work partials; [16, 28) int64 phase stamps; [kMetaWork + lblk(a, b)
+// * kPlanShardMax + s] edges of the patches whose free poses hold a and b, from
+// shard s (ba_window_kernel gives each lower block workgroups in proportion;
+// a block's 16 shard counts are one 64-B run: four 16-B loads)
 constexpr int kWMaxNB = kWMaxN * (kWMaxN + 1) / 2;
 constexpr int kPlanShardMax = 16;
 constexpr int kMetaWork = 64;
@@ -262,7 +263,7 @@ __device__ __forceinline__ void plan_block_work(int n, F patch, int* wl) {
 __device__ __forceinline__ void plan_store_work(const Plan& plan, const int* wl, int s, int N) {
   const int nb = N * (N + 1) / 2;
   for (int t = threadIdx.x; t < nb; t += blockDim.x)
-    plan.meta[kMetaWork + s * kWMaxNB + t] = wl[t];
+    plan.meta[kMetaWork + t * kPlanShardMax + s] = wl[t];
 }
 
 __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
@@ -1196,10 +1197,17 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       const int o = min(2 * lane + h, nlow - 1);  // clamped: loads stay unconditional
       int ja = 1;
       while ((ja + 1) * ja / 2 <= o) ja++;
-      const int* src = A.plan.meta + kMetaWork + o + ja;  // lblk(ja, jb) = o + ja
+      const int4* src = reinterpret_cast<const int4*>(
+          A.plan.meta + kMetaWork + (o + ja) * kPlanShardMax);  // lblk(ja, jb) = o + ja
       int wq[kPlanShardMax];
 #pragma unroll
-      for (int q = 0; q < kPlanShardMax; q++) wq[q] = src[q * kWMaxNB];
+      for (int q4 = 0; q4 < kPlanShardMax / 4; q4++) {
+        const int4 v = src[q4];
+        wq[4 * q4] = v.x;
+        wq[4 * q4 + 1] = v.y;
+        wq[4 * q4 + 2] = v.z;
+        wq[4 * q4 + 3] = v.w;
+      }
       int w = 0;
 #pragma unroll
       for (int q = 0; q < kPlanShardMax; q++) w += q < nsh ? wq[q] : 0;

@@ -258,12 +258,12 @@ def _host_grouping(ii, jj, kk, t0, t1):
 
 
 def _check_block_work(meta, ref, N):
-    """The sharded plan's block work (meta[64 + s * 136 + lblk(a, b)], shards
+    """The sharded plan's block work (meta[64 + lblk(a, b) * 16 + s], shards
     s < meta[3]): edges of the patches whose free-pose mask holds a and b."""
     nsh = int(meta[3])
     if nsh == 0:  # single-workgroup plan: no partials (the kernel splits evenly)
         return
-    got = meta[64:64 + 16 * 136].reshape(16, 136)[:nsh].sum(0)
+    got = meta[64:64 + 16 * 136].reshape(136, 16)[:, :nsh].sum(1)
     want = np.zeros(136, np.int64)
     poff, pmask = ref[1], ref[2]
     for u in range(pmask.size):
