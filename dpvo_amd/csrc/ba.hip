@@ -32,6 +32,7 @@
 //   same code without / as the solve tail: the edge-sharded multi-GPU form
 //   (SURVEY 8e).
 #include "common.hpp"
+#include "ba_device.hpp"  // bad::lin_edge: the one copy of the edge math
 
 namespace dpvo {
 
@@ -375,53 +376,33 @@ __global__ void __launch_bounds__(kSetupThreads) ba_setup_kernel(BaArgs A, BaWs 
 }
 
 #pragma clang fp contract(off)
+// The multi-kernel path's record layout [w(2), r(2), Jz(2), Ji(2x6), Jj(2x6)]
+// over bad::lin_edge (ba_device.hpp), the same edge math the window kernel
+// runs (ba_cuda.cu:265-333); only the patch-centre normalisation is here.
 __device__ __forceinline__ void edge_linearize(const float* poses, const float* patches, int P,
                                                float fx, float fy, float cx, float cy, float tx,
                                                float ty, float wx, float wy, int ix, int jx,
                                                int64_t kx, bool use_depth, float depth, float* o) {
-  const float* pi = poses + 7 * (size_t)ix;
-  const float* pj = poses + 7 * (size_t)jx;
   const float* pk = patches + (size_t)kx * 3 * P * P;
   const int c11 = P + 1;  // patches[kx][*][1][1]  (ba_cuda.cu:282-285)
-  float ti[3] = {pi[0], pi[1], pi[2]}, qi[4] = {pi[3], pi[4], pi[5], pi[6]};
-  float tj[3] = {pj[0], pj[1], pj[2]}, qj[4] = {pj[3], pj[4], pj[5], pj[6]};
-  float Xi[4], Xj[4];
-  Xi[0] = (pk[c11] - cx) / fx;
-  Xi[1] = (pk[P * P + c11] - cy) / fy;
-  Xi[2] = 1.0f;
-  Xi[3] = use_depth ? depth : pk[2 * P * P + c11];
-  float tij[3], qij[4];
-  relSE3(ti, qi, tj, qj, tij, qij);
-  actSE3(tij, qij, Xi, Xj);
-  const float X = Xj[0], Y = Xj[1], Z = Xj[2], W = Xj[3];
-  const float d = ((double)Z >= 0.2) ? (float)(1.0 / (double)Z) : 0.0f;  // ba_cuda.cu:296
-  const float d2 = d * d;
-  const float x1 = fx * (X / Z) + cx;
-  const float y1 = fy * (Y / Z) + cy;
-  const float rx = tx - x1, ry = ty - y1;
-  const bool in_bounds = (sqrtf(rx * rx + ry * ry) < 128.0f) && ((double)Z > 0.2) &&
-                         (x1 > -64.0f) && (y1 > -64.0f) && (x1 < 2.0f * cx + 64.0f) &&
-                         (y1 < 2.0f * cy + 64.0f);  // :305-306
-  const float mask = in_bounds ? 1.0f : 0.0f;
-  float Jj0[6] = {fx * W * d, 0.0f, fx * -X * W * d2, fx * -X * Y * d2, fx * (1 + X * X * d2),
-                  fx * -Y * d};
-  float Jj1[6] = {0.0f, fy * W * d, fy * -Y * W * d2, fy * (-1 - Y * Y * d2), fy * (X * Y * d2),
-                  fy * X * d};
-  float Ji0[6], Ji1[6];
-  adjSE3(tij, qij, Jj0, Ji0);
-  adjSE3(tij, qij, Jj1, Ji1);
-  o[0] = mask * wx;
-  o[1] = mask * wy;
-  o[2] = tx - x1;
-  o[3] = ty - y1;
-  o[4] = fx * (tij[0] * d - tij[2] * (X * d2));
-  o[5] = fy * (tij[1] * d - tij[2] * (Y * d2));
+  const float nx = (pk[c11] - cx) / fx;
+  const float ny = (pk[P * P + c11] - cy) / fy;
+  const float dz = use_depth ? depth : pk[2 * P * P + c11];
+  bad::Lin L;
+  bad::lin_edge(poses + 7 * (size_t)ix, poses + 7 * (size_t)jx, nx, ny, dz, tx, ty, wx, wy, fx, fy,
+                cx, cy, L);
+  o[0] = L.w[0];
+  o[1] = L.w[1];
+  o[2] = L.r[0];
+  o[3] = L.r[1];
+  o[4] = L.Jz[0];
+  o[5] = L.Jz[1];
 #pragma unroll
   for (int a = 0; a < 6; a++) {
-    o[6 + a] = Ji0[a];
-    o[12 + a] = Ji1[a];
-    o[18 + a] = Jj0[a];
-    o[24 + a] = Jj1[a];
+    o[6 + a] = L.Ji[0][a];
+    o[12 + a] = L.Ji[1][a];
+    o[18 + a] = L.Jj[0][a];
+    o[24 + a] = L.Jj[1][a];
   }
 }
 
