@@ -26,6 +26,7 @@ Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -114,9 +115,25 @@ def launch_ranks(n, argv, cmd=None):
 
     cmd = cmd or [sys.executable, os.path.abspath(__file__), *argv]
     procs = [subprocess.Popen(cmd, env=e) for e in rank_envs(n, free_port())]
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    # poll: a rank that fails (e.g. before or inside init_process_group) ends the
+    # run at once instead of leaving the others in rendezvous until its timeout
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc is not None and rc != 0]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return bad[0]
+        if all(rc is not None for rc in rcs):
+            return 0
+        time.sleep(0.05)
 
 
 def warm_until(step_fn, torch, min_ms=200.0, max_steps=100000):
@@ -395,21 +412,59 @@ def main():
             step(0)
         graph.replay()
         torch.cuda.synchronize()
-        warm_until(lambda i: graph.replay(), torch, args.warm_ms)
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
+    # The host call of the first timed step used to take ~0.22 ms (against
+    # ~0.03 ms for the others; step_split.host_enqueue_ms_first) with the GPU
+    # idle meanwhile -- 7 % of a 20-step run, the driver-vs-long-run gap of
+    # VERDICT r04 weak 2.  The roofline bookkeeping above (torch sorts, .item()
+    # syncs, fresh Python objects) ran right before it; now a garbage
+    # collection and a second (short) time-based warm-up come last.
+    gc.collect()
+    warm_until(step if graph is None else (lambda i: graph.replay()), torch,
+               min(50.0, args.warm_ms))
+
+    def run_one(i):
         if graph is not None:
             graph.replay()
         else:
             step(i)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    host_s = [0.0] * args.steps
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        h = time.perf_counter()
+        run_one(i)
+        host_s[i] = time.perf_counter() - h  # host enqueue time of the step (no sync)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+
+    # per-step split, in a second pass of the same length
+    # right after the timed one (events are not recorded inside the timed loop):
+    # HIP events before / after each step on the launch stream = the GPU time
+    # of the step's kernels incl. the gaps between them; host enqueue = the
+    # wall time of the Python call (perf_counter, no sync) in the timed loop
+    n_pp = max(args.steps, 20)
+    pev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(n_pp)]
+    for i in range(n_pp):
+        pev[i][0].record()
+        run_one(i)
+        pev[i][1].record()
+    torch.cuda.synchronize()
+    gpu_ms = sorted(a.elapsed_time(b) for a, b in pev)
+    host_ms = sorted(1e3 * h for h in host_s)
+    step_split = {
+        "gpu_ms_median": gpu_ms[n_pp // 2], "gpu_ms_min": gpu_ms[0], "gpu_ms_max": gpu_ms[-1],
+        "host_enqueue_ms_median": host_ms[len(host_ms) // 2], "host_enqueue_ms_max": host_ms[-1],
+        "host_enqueue_ms_first": 1e3 * host_s[0],
+        "note": "gpu = HIP events around each step (second pass, same length); host = "
+                "perf_counter around each timed step() call without a sync",
+    }
 
     # every BA call of the run (warmup, event steps, graph replays) finished
     # without a fatal status (raises RuntimeError otherwise)
@@ -469,6 +524,7 @@ def main():
             "warmup": args.warmup,
             "warm_ms": args.warm_ms,
             "ms_per_step": 1e3 * elapsed / args.steps,
+            "step_split": step_split,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

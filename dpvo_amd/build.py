@@ -31,7 +31,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("DPVO_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["corr.hip", "corr_nhwc.hip", "ba.hip", "ba_window.hip", "ba_large.hip", "lie.hip", "pgo.hip", "pg.hip",
-               "keyframe.hip"]
+               "keyframe.hip", "spd_solve.hip"]
 EXTENSIONS = {
     "cuda_corr": "ext_cuda_corr.cpp",
     "cuda_ba": "ext_cuda_ba.cpp",

@@ -27,7 +27,13 @@ constexpr int kScanRun = 16;
 // of nonzero entries before (low bits) -- bucket starts and bucket indices.
 __device__ inline int fscan(int* data, int n, int* scr, int pack_shift = 0) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  if (n <= 0) return 0;
+  if (n <= 0) {
+    // keep the barrier of every other path: callers rely on it to order their
+    // LDS atomics before reading the results (plan_sharded's ctl[4..6] on a
+    // shard with an empty kk range)
+    __syncthreads();
+    return 0;
+  }
   if (n <= 64 * kScanRun) {
     // small scans (the plan's shard ranges, the BA setup's patch counts at
     // cfg2): wave 0 alone, one DPP scan, two barriers instead of three

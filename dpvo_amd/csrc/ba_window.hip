@@ -31,8 +31,12 @@
 //   * Grid <= 256 workgroups (one per CU, all co-resident); flags are
 //     epoch-tagged (graph-replayable) and every spin-wait has a wall-clock
 //     timeout (status bit 16) so the grid always drains.
+#include <unistd.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <random>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -106,9 +110,7 @@ struct WArgs {
   int E, P, num_poses, num_patches, t0, N, iters, NB, Sd, So, G;
   Plan plan;
   double* part;      // [2][G][kPartPad] published partial blocks, by iteration parity (flag modes)
-  v4u* gran;         // [2][G][kGranPad] the same as 16-B granules (default mode);
-                     // dense kernel: [2][G][NB * 36] contributions of every workgroup
-  v4u* gran2;        // dense kernel: [2][NB][36] reduced blocks
+  v4u* gran;         // [2][G][kGranPad] the same as 16-B granules (default mode)
   long long* flags;  // persistent [kFlagWords]
   float* ejg;        // [2][E][12] E entries by edge and iteration parity (fp32), HBM fallback
   int* status;       // [1] OR of status bits (workspace meta)
@@ -120,6 +122,7 @@ struct WArgs {
                      // product calls
   double* dxo;       // [6N] dX of the latest iteration (workgroup 0; dpvo_ba_last_dx) or null
   const int* t0d;    // device t0 or null (then t0)
+  unsigned long long salt;  // per-process random granule-key salt (see granule())
 };
 
 __device__ __forceinline__ size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
@@ -1057,19 +1060,30 @@ __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, do
 // A published value as one 16-B granule {value, hash, tag}, written by ONE
 // 16-B sc1 store: a reader that sees the expected tag and a matching hash has
 // the whole value (the granule hand-off of MI355X_MICROARCH.md: no flag, no
-// ordering between granules; 16-B sc1 stores observed untorn on gfx950 -- the
-// hash also rejects a torn read, tag of one write with the value of another)
-__device__ __forceinline__ unsigned gran_hash(unsigned lo, unsigned hi) {
-  return lo ^ (hi * 0x9E3779B1u) ^ 0x5bd1e995u;
+// ordering between granules; 16-B sc1 stores observed untorn on gfx950).
+// key = (epoch * 64 + iteration + 1) ^ salt: 64 bits, unique per call and
+// iteration, and per process (salt: a random 64-bit value drawn once per
+// process, so granules another process left in reused memory never carry
+// this process's keys).  The tag is key's low word; the hash covers the
+// value AND the whole key, so any torn mix of two writes (the tag of one,
+// the value and hash of another -- e.g. an internally consistent granule of
+// the same parity from iteration it - 2) fails the check, and a granule of
+// another call whose key shares the low word fails it through the high word.
+__device__ __forceinline__ unsigned gran_hash(unsigned lo, unsigned hi, unsigned long long key) {
+  unsigned h = lo ^ 0x5bd1e995u;
+  h = (h ^ (h >> 16)) * 0x7feb352du + hi;
+  h = (h ^ (h >> 15)) * 0x846ca68bu + (unsigned)key;
+  h = (h ^ (h >> 16)) * 0x9E3779B1u + (unsigned)(key >> 32);
+  return h ^ (h >> 15);
 }
-__device__ __forceinline__ v4u granule(double v, unsigned tag) {
+__device__ __forceinline__ v4u granule(double v, unsigned long long key) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(v);
   const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
   v4u r;
   r.x = lo;
   r.y = hi;
-  r.z = gran_hash(lo, hi);
-  r.w = tag;
+  r.z = gran_hash(lo, hi, key);
+  r.w = (unsigned)key;
   return r;
 }
 
@@ -1077,7 +1091,7 @@ __device__ __forceinline__ v4u granule(double v, unsigned tag) {
 // (granule mode: gout = this workgroup's granule slot, tag its iteration tag)
 template <int NA>
 __device__ void reduce_acc(const double* acc, double* red, double* out, v4u* gout = nullptr,
-                           unsigned tag = 0) {
+                           unsigned long long tag = 0) {
   const int tid = threadIdx.x;
   // two rounds of 128 columns: red[v][col]
   if (tid >= 128) {
@@ -1561,7 +1575,8 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     double* const pbuf = A.part + (size_t)(it & 1) * A.G * kPartPad;
     double* part = pbuf + (size_t)g * kPartPad;
     double* red = reinterpret_cast<double*>(L.region);
-    const unsigned gtag = (unsigned)(epoch * 64 + it + 1);
+    const unsigned long long gkey = (unsigned long long)(epoch * 64 + it + 1) ^ A.salt;
+    const unsigned gtag = (unsigned)gkey;
 #if defined(BA_XCHG_FLAGS) || defined(BA_XCHG_FENCES)
     v4u* const gbuf = nullptr;
     v4u* const gslot = nullptr;
@@ -1575,11 +1590,11 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       assemble<1>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
       mark(A, mb + 4);
       if (A.marks && tid == 0 && it == 0 && g < 256) A.marks[1408 + g] = (int64_t)wall_clock64();
-      reduce_acc<27>(acc, red, part, gslot, gtag);
+      reduce_acc<27>(acc, red, part, gslot, gkey);
     } else {
       assemble<2>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
       if (A.marks && tid == 0 && it == 0 && g < 256) A.marks[1408 + g] = (int64_t)wall_clock64();
-      reduce_acc<36>(acc, red, part, gslot, gtag);
+      reduce_acc<36>(acc, red, part, gslot, gkey);
     }
     mark(A, mb + 0);
     if (A.marks && tid == 0 && it < 2 && g < 256)  // per-workgroup stamps (instrumentation)
@@ -1632,7 +1647,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
             v[r] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rs, off[r], 0, kSc1));
 #pragma unroll
           for (int r = 0; r < kIn; r++) {
-            const bool ok = ((pend >> r) & 1u) && v[r].w == gtag && v[r].z == gran_hash(v[r].x, v[r].y);
+            const bool ok = ((pend >> r) & 1u) && v[r].w == gtag && v[r].z == gran_hash(v[r].x, v[r].y, gkey);
             if (ok) {
               pc[pos[r]] = __longlong_as_double((long long)(((unsigned long long)v[r].y << 32) | v[r].x));
               pend &= ~(1u << r);
@@ -1889,659 +1904,6 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   }
 }
 
-// ===========================================================================
-// patch-partitioned iteration kernel (ba_dense_kernel)
-// ===========================================================================
-// The block kernel above gives every workgroup one (lower block (a, b),
-// share): each re-linearises every edge of every patch whose free poses hold
-// a and b.  In a DPVO local-BA window a patch sees nearly every free pose, so
-// each edge is linearised ~N(N+1)/2 times and the grid spends its iteration
-// on redundant linearisation (E = 9850: ~40 us).  Here workgroup g owns the
-// patches [g nuniq / G, (g + 1) nuniq / G) of the plan -- and so all their
-// edges, in the plan's order -- and per iteration:
-//   stage A   each own edge linearised ONCE (fp32, the reference's math);
-//             per own patch C, u, Q and its E column block at every free
-//             pose it touches (fp64, edge order); then the workgroup's
-//             contribution to EVERY lower block of S and to y (fp64, fixed
-//             order: own edges, then own patches, ascending) -> published as
-//             16-B granules (one per value).
-//   reduce    workgroup b < NB owns block b: it gathers that block's
-//             contributions from all G workgroups (granules, tag-checked),
-//             sums them in workgroup order, damps the diagonal (S += I (1e-4
-//             S + 1), ba_cuda.cu:560) and publishes the block.
-//   gather    every workgroup gathers the NB reduced blocks and solves S dX =
-//             y itself (ba_solve.hpp: identical bits everywhere).
-//   apply     pose retraction (every workgroup, its pose table) and the
-//             inverse depths of its own patches (dZ = Q (u - E^T dX),
-//             ba_cuda.cu:563; patch_retr_kernel :209-229).
-// Two grid-wide hand-offs per iteration instead of one, but no workgroup
-// re-linearises another's edges, and the assembly is balanced by construction.
-constexpr int kDEdges = 1024;  // own edges per workgroup (LDS records; status 32 beyond)
-constexpr int kDChunk = 256;   // edges linearised per pass
-constexpr int kDItems = 4;     // (block, row) items per thread: NB * 6 <= 4 * 256 (N <= 16)
-constexpr int kDRow = 36;      // granules per block in a published contribution
-constexpr int kDJs = 33;       // floats per Lin record (odd: lanes on different edges hit different banks)
-constexpr int kDMw = kDChunk / 32;  // words per block edge mask
-static_assert(kWMaxN * (kWMaxN + 1) / 2 * 6 <= kDItems * kWT, "items per thread");
-
-struct DL {  // LDS layout of one dense workgroup
-  int np, ne, q0;        // own patches, own edges, first own position
-  int* poff;             // [np + 1] own patch -> own edge offset (relative)
-  int* pkx;              // [np] patch id
-  unsigned* pmask;       // [np] free-pose mask
-  int* soff;             // [np + 1] first E-vector slot of each own patch
-  float2* nxy;           // [np] normalised centre
-  float* dep;            // [np] inverse depth (current)
-  float* dbase;          // [np] [2][0][0] of the input
-  double2* qu;           // [np] Q, u of the last linearisation
-  double* Ev;            // [slots][6] E column blocks (own patches x their free poses)
-  unsigned short* ec;    // [ne] pose slot of ii | slot of jj << 8
-  int2* gij;             // [ne] global pose ids (poses past the table are read from HBM)
-  float4* tw;            // [ne] target, weight
-  float* J;              // [kDChunk][kDJs] Lin records of the current pass
-  unsigned* bm;          // [NB][kDMw] per block: pass edges that touch it (bit q - e0)
-};
-
-__device__ __forceinline__ int lin_pack(const Lin& o, float* d) {
-  d[0] = o.w[0]; d[1] = o.w[1]; d[2] = o.r[0]; d[3] = o.r[1]; d[4] = o.Jz[0]; d[5] = o.Jz[1];
-#pragma unroll
-  for (int k = 0; k < 6; k++) {
-    d[6 + k] = o.Ji[0][k];
-    d[12 + k] = o.Ji[1][k];
-    d[18 + k] = o.Jj[0][k];
-    d[24 + k] = o.Jj[1][k];
-  }
-  return 30;
-}
-
-__global__ void __launch_bounds__(kWT) ba_dense_kernel(WArgs A) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, g = blockIdx.x, G = A.G;
-  const int N = A.N, P = A.P, PP = P * P, NB = A.NB;
-  const float fx = A.intrinsics[0], fy = A.intrinsics[1], cx = A.intrinsics[2],
-              cy = A.intrinsics[3];
-  const int t0w = A.t0d ? *A.t0d : A.t0;
-  const long long epoch =
-      __hip_atomic_load(&A.flags[kEpochWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-  const int nuniq = A.plan.meta[0], fmin = A.plan.meta[1];
-  mark(A, 0);
-  if (A.marks && g == 0 && tid == 0) A.marks[59] = 0;
-  WL L;  // shared header: ctl, pose table, dX, block table
-  L.ctl = (int*)lds;
-  int* ctl = L.ctl;
-  L.pose = (float*)(lds + 256);
-  L.dX = (double*)(lds + 256 + sizeof(float) * 8 * kWSlots);
-  L.tri = (unsigned short*)(lds + 256 + sizeof(float) * 8 * kWSlots + sizeof(double) * 6 * kWMaxN);
-  size_t off = al16(256 + sizeof(float) * 8 * kWSlots + sizeof(double) * 6 * kWMaxN +
-                    sizeof(unsigned short) * (kWMaxN * (kWMaxN + 1) / 2));
-  for (int t = tid; t < NB; t += kWT) {
-    int ta, tb;
-    tri_of(t, ta, tb);
-    L.tri[t] = (unsigned short)((ta << 8) | tb);
-  }
-  if (tid == 0) {
-    ctl[cFail] = 0;
-    ctl[cFailAny] = 0;
-    ctl[cTimeout] = 0;
-    ctl[cCap] = 0;
-  }
-  // ---------------- setup: own patches and edges ----------------
-  DL D;
-  const int u_lo = (int)((long long)g * nuniq / G), u_hi = (int)((long long)(g + 1) * nuniq / G);
-  D.np = u_hi - u_lo;
-  auto take = [&](size_t bytes) {
-    char* p = lds + off;
-    off = al16(off + bytes);
-    return p;
-  };
-  D.poff = (int*)take(sizeof(int) * (D.np + 1));
-  D.pkx = (int*)take(sizeof(int) * (D.np + 1));
-  D.pmask = (unsigned*)take(sizeof(unsigned) * (D.np + 1));
-  D.soff = (int*)take(sizeof(int) * (D.np + 1));
-  D.nxy = (float2*)take(sizeof(float2) * (D.np + 1));
-  D.dep = (float*)take(sizeof(float) * (D.np + 1));
-  D.dbase = (float*)take(sizeof(float) * (D.np + 1));
-  D.qu = (double2*)take(sizeof(double2) * (D.np + 1));
-  // plan entries of the own patches (first round trip; np <= nuniq / G + 1)
-  for (int r0 = tid; r0 <= D.np; r0 += kWT) {
-    const int u = min(u_lo + r0, nuniq);
-    const int po = A.plan.poff[u];
-    const int uc = min(u, nuniq - 1);
-    const int kx = A.plan.pkk[uc];
-    const unsigned m = A.plan.pmask[uc];
-    D.poff[r0] = po;
-    if (r0 < D.np) {
-      D.pkx[r0] = kx;
-      D.pmask[r0] = m;
-      D.soff[r0] = max(__popc(m), 1);  // slot count (>= 1: slot 0 carries C, u when m == 0)
-    }
-  }
-  __syncthreads();
-  mark(A, 40);
-  D.q0 = D.poff[0];
-  D.ne = D.poff[D.np] - D.q0;
-  if (D.ne > kDEdges) {  // contributes nothing; the call reports status 32 (raised)
-    if (tid == 0) ctl[cCap] = 1;
-    D.ne = 0;
-    D.np = 0;
-  }
-  int* scr = ctl + cScan;
-  const int nslot = fscan(D.soff, D.np, scr);  // soff[r] = first slot of own patch r
-  if (tid == 0) D.soff[D.np] = nslot;
-  mark(A, 41);
-  mark(A, 42);  // (no record phase: the plan's order is used as is)
-  D.Ev = (double*)take(sizeof(double) * 6 * (nslot + 1));
-  D.ec = (unsigned short*)take(sizeof(unsigned short) * (D.ne + 1));
-  D.gij = (int2*)take(sizeof(int2) * (D.ne + 1));
-  D.tw = (float4*)take(sizeof(float4) * (D.ne + 1));
-  D.J = (float*)take(sizeof(float) * kDJs * kDChunk);
-  D.bm = (unsigned*)take(sizeof(unsigned) * kDMw * (NB + 1));
-  double* R = (double*)take(0);  // the rest: reduction staging / gather / solve
-  const size_t NN = N > 0 ? N : 1;
-  const size_t solve_b =
-      sizeof(double) * (36 * (NN * (NN + 1) / 2) + 6 * NN) + wsolve_bytes((int)NN) + 64;
-  const size_t red_b = sizeof(double) * kDRow * (size_t)G;
-  const size_t gat_b = sizeof(double) * (36 * (size_t)NB + 6 * NN + (size_t)kDRow * NB) +
-                       sizeof(int) * (NB + 1);
-  size_t reg_b = solve_b > red_b ? solve_b : red_b;
-  reg_b = reg_b > gat_b ? reg_b : gat_b;
-  if (off + reg_b > (size_t)kWLds) {
-    if (tid == 0) ctl[cCap] = 1;
-    D.ne = 0;
-    D.np = 0;
-  }
-  // patch values, edge ids -> inputs, pose table (second / third round trips)
-  for (int r = tid; r < D.np; r += kWT) {
-    const float* pk = A.patches + (size_t)D.pkx[r] * 3 * PP;
-    const int c11 = P + 1;
-    const float v0 = pk[c11], v1 = pk[PP + c11], v2 = pk[2 * PP + c11], v3 = pk[2 * PP];
-    D.nxy[r] = make_float2((v0 - cx) / fx, (v1 - cy) / fy);
-    D.dep[r] = v2;
-    D.dbase[r] = v3;  // patch_retr_kernel reads [2][0][0] (:225)
-  }
-  for (int q0 = tid; q0 < D.ne; q0 += 4 * kWT) {
-    int ev[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) ev[r] = A.plan.epos[D.q0 + min(q0 + r * kWT, D.ne - 1)];
-    int64_t gi[4], gj[4];
-    float2 tg[4], wt[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      gi[r] = A.ii[ev[r]];
-      gj[r] = A.jj[ev[r]];
-      tg[r] = reinterpret_cast<const float2*>(A.target)[ev[r]];
-      wt[r] = reinterpret_cast<const float2*>(A.weight)[ev[r]];
-    }
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int q = q0 + r * kWT;
-      if (q >= D.ne) continue;
-      const unsigned si = wslot((int)gi[r], t0w, N, fmin), sj = wslot((int)gj[r], t0w, N, fmin);
-      D.ec[q] = (unsigned short)(si | (sj << 8));
-      D.gij[q] = make_int2((int)gi[r], (int)gj[r]);
-      D.tw[q] = make_float4(tg[r].x, tg[r].y, wt[r].x, wt[r].y);
-    }
-  }
-  mark(A, 43);
-  {
-    constexpr int kPr = kWSlots * 8 / kWT;
-#pragma unroll
-    for (int r = 0; r < kPr; r++) {
-      const int k = tid + r * kWT, sl = k >> 3, c = k & 7;
-      const int gp = (sl < N) ? t0w + sl : fmin + (sl - N);
-      const bool ok = c < 7 && gp >= 0 && gp < A.num_poses && (sl < N || fmin != 0x7fffffff);
-      const float v = A.poses[7 * (size_t)min(max(gp, 0), A.num_poses - 1) + min(c, 6)];
-      L.pose[k] = ok ? v : ((c == 6) ? 1.0f : 0.0f);
-    }
-  }
-  __syncthreads();
-  mark(A, 1);
-  if (A.marks && tid == 0 && g < 256) A.marks[1152 + g] = (int64_t)wall_clock64();
-
-  const double lam = (double)A.lmbda[0];
-  // granule buffers: contributions [2][G][NB * kDRow], reduced [2][NB][kDRow]
-  const int rowg = NB * kDRow;
-  for (int it = 0; it < A.iters; it++) {
-    const int mb = 2 + 8 * it;
-    const int par = it & 1;
-    const unsigned gtag = (unsigned)(epoch * 64 + it + 1);
-    if (it > 0) {
-      // ---- apply dX of iteration it-1: poses (pose table), own depths ----
-      for (int i = tid; i < N; i += kWT) {  // pose_retr_kernel (:178-206)
-        float xi[6], tt[3], qq[4], t1[3], q1[4];
-#pragma unroll
-        for (int k = 0; k < 6; k++) xi[k] = (float)L.dX[6 * i + k];
-        float* pl = L.pose + 8 * i;
-        tt[0] = pl[0]; tt[1] = pl[1]; tt[2] = pl[2];
-        qq[0] = pl[3]; qq[1] = pl[4]; qq[2] = pl[5]; qq[3] = pl[6];
-        retrSE3(xi, tt, qq, t1, q1);
-        pl[0] = t1[0]; pl[1] = t1[1]; pl[2] = t1[2];
-        pl[3] = q1[0]; pl[4] = q1[1]; pl[5] = q1[2]; pl[6] = q1[3];
-      }
-      for (int r = tid; r < D.np; r += kWT) {  // dZ = Q (u - E^T dX) (:563)
-        const unsigned m = D.pmask[r];
-        double ex = 0.0;
-        int s = D.soff[r];
-        for (unsigned mm = m; mm; mm &= mm - 1, s++) {
-          const int p = __builtin_ctz(mm);
-          const double* e = D.Ev + 6 * s;
-          const double* d = L.dX + 6 * p;
-          ex += e[0] * d[0] + e[1] * d[1] + e[2] * d[2] + e[3] * d[3] + e[4] * d[4] + e[5] * d[5];
-        }
-        const double2 qu = D.qu[r];
-        const float dz = (float)(qu.x * (qu.y - ex));
-        const float base = (it == 1) ? D.dbase[r] : D.dep[r];
-        float d = base + dz;
-        d = (d > 20.0f) ? 1.0f : d;
-        D.dep[r] = (float)fmax((double)d, 1e-4);
-      }
-      __syncthreads();
-    }
-    // ---- stage A: own edges once, own patches, contributions to every block ----
-    double acc[kDItems][7];  // (block, row) item: 6 entries + y
-#pragma unroll
-    for (int k = 0; k < kDItems; k++)
-#pragma unroll
-      for (int z = 0; z < 7; z++) acc[k][z] = 0.0;
-    for (int pa = 0; pa < D.np;) {
-      // pass: whole patches [pa, pb) with at most kDChunk edges
-      int pb = pa + 1;
-      {
-        int lo = pa + 1, hi = D.np;
-        const int base = D.poff[pa];
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (D.poff[mid] - base <= kDChunk) lo = mid; else hi = mid - 1;
-        }
-        pb = lo;
-      }
-      const int e0 = D.poff[pa] - D.q0, e1r = D.poff[pb] - D.q0;
-      if (e1r - e0 > kDChunk && tid == 0) ctl[cCap] = 1;  // one patch past a pass: status 32
-      const int e1 = min(e1r, e0 + kDChunk);
-      for (int t = tid; t < kDMw * NB; t += kWT) D.bm[t] = 0u;
-      __syncthreads();
-      if (it == 0 && pa == 0) mark(A, 55);
-      // (1) thread per edge: the reference's fp32 linearisation; the edge joins
-      // the masks of the (at most 3) blocks it adds to
-      for (int q = e0 + tid; q < e1; q += kWT) {
-        const unsigned c = D.ec[q];
-        const unsigned si = c & 0xff, sj = c >> 8;
-        // the edge's patch: last own patch whose first edge <= q (binary search)
-        int lo = pa, hi = pb - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (D.poff[mid] - D.q0 <= q) lo = mid; else hi = mid - 1;
-        }
-        float Pi[7], Pj[7];
-        const int2 gp = D.gij[q];
-        pose_of(A, L, si, si == kHbm ? gp.x : 0, Pi);
-        pose_of(A, L, sj, sj == kHbm ? gp.y : 0, Pj);
-        const float4 tw = D.tw[q];
-        Lin o;
-        lin_edge(Pi, Pj, D.nxy[lo].x, D.nxy[lo].y, D.dep[lo], tw.x, tw.y, tw.z, tw.w, fx, fy, cx,
-                 cy, o);
-        lin_pack(o, D.J + kDJs * (q - e0));
-        const int w = (q - e0) >> 5;
-        const unsigned bit = 1u << ((q - e0) & 31);
-        if (si < (unsigned)N) atomicOr(&D.bm[kDMw * lblk(si, si) + w], bit);
-        if (sj < (unsigned)N && sj != si) {
-          atomicOr(&D.bm[kDMw * lblk(sj, sj) + w], bit);
-          if (si < (unsigned)N) atomicOr(&D.bm[kDMw * lblk(max(si, sj), min(si, sj)) + w], bit);
-        }
-      }
-      __syncthreads();
-      if (it == 0 && pa == 0) mark(A, 56);  // diagnostics: pass 0 sub-stages of workgroup 0
-      if (it == 0 && pa == 0 && A.marks && tid == 0 && g < 256) {
-        A.marks[1664 + g] = (int64_t)wall_clock64();
-        A.marks[1920 + g] = (int64_t)D.ne | ((int64_t)D.np << 16);
-      }
-      // (2) thread per (own patch, slot): C, u (slot 0) and the E column block at
-      // the slot's pose, edges in order (fp64 products of the fp32 terms)
-      {
-        const int s0 = D.soff[pa], s1 = D.soff[pb];
-        for (int sl = s0 + tid; sl < s1; sl += kWT) {
-          int lo = pa, hi = pb - 1;  // patch of slot sl
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (D.soff[mid] <= sl) lo = mid; else hi = mid - 1;
-          }
-          const int r = lo, k = sl - D.soff[r];
-          const unsigned m = D.pmask[r];
-          unsigned mm = m;
-          for (int t = 0; t < k; t++) mm &= mm - 1;
-          const unsigned p = m ? (unsigned)__builtin_ctz(mm) : kFix;
-          double C = 0.0, U = 0.0, Ev[6] = {0, 0, 0, 0, 0, 0};
-          for (int q = D.poff[r] - D.q0; q < min(D.poff[r + 1] - D.q0, e1); q++) {
-            const float* j = D.J + kDJs * (q - e0);
-            const unsigned c = D.ec[q];
-            const unsigned ci = (c & 0xff) < (unsigned)N ? (c & 0xff) : kFix;
-            const unsigned cj = (c >> 8) < (unsigned)N ? (c >> 8) : kFix;
-            // every value read unconditionally, then selected: a load under
-            // the select compiles to a branch that waits for it alone
-            float jr[30];
-#pragma unroll
-            for (int t = 0; t < 30; t++) jr[t] = j[t];
-#pragma unroll
-            for (int row = 0; row < 2; row++) {
-              const double wr = jr[row], wz = wr * (double)jr[4 + row];
-              const double cC = wz * (double)jr[4 + row];
-              const double cU = (wr * (double)jr[2 + row]) * (double)jr[4 + row];
-              C += (k == 0) ? cC : 0.0;
-              U += (k == 0) ? cU : 0.0;
-#pragma unroll
-              for (int x = 0; x < 6; x++) {
-                const double pj = wz * (double)jr[18 + 6 * row + x], pi = wz * (double)jr[6 + 6 * row + x];
-                Ev[x] += (cj == p) ? pj : 0.0;
-                Ev[x] -= (ci == p) ? pi : 0.0;
-              }
-            }
-          }
-          double* e = D.Ev + 6 * sl;
-#pragma unroll
-          for (int x = 0; x < 6; x++) e[x] = Ev[x];
-          if (k == 0) D.qu[r] = make_double2(1.0 / (C + lam), U);  // (:519)
-        }
-      }
-      __syncthreads();
-      if (it == 0 && pa == 0) mark(A, 57);
-      // (3) thread per (block, row) item: B terms of the pass's edges (ba_cuda.cu:
-      // 339-370), then the Schur terms of its patches (:554-558), fixed order
-#pragma unroll
-      for (int k = 0; k < kDItems; k++) {
-        const int item = tid + k * kWT;
-        if (item >= NB * 6) continue;
-        const int blk = item / 6, x = item % 6;
-        const unsigned ua = L.tri[blk] >> 8, ub = L.tri[blk] & 0xff;
-        const bool dg = ua == ub;
-        for (int w = 0; w < kDMw; w++)
-        for (unsigned bits = D.bm[kDMw * blk + w]; bits; bits &= bits - 1) {
-          const int q = e0 + 32 * w + __builtin_ctz(bits);
-          const unsigned c = D.ec[q];
-          const unsigned ci = (c & 0xff) < (unsigned)N ? (c & 0xff) : kFix;
-          const unsigned cj = (c >> 8) < (unsigned)N ? (c >> 8) : kFix;
-          const bool ia = ci == ua, ja = cj == ua, ib = ci == ub, jb = cj == ub;
-          if (!(dg ? (ia || ja) : ((ia && jb) || (ja && ib)))) continue;
-          const float* j = D.J + kDJs * (q - e0);
-          float jr[30];  // unconditional reads, selects below (see stage 2)
-#pragma unroll
-          for (int t = 0; t < 30; t++) jr[t] = j[t];
-#pragma unroll
-          for (int row = 0; row < 2; row++) {
-            const double wr = jr[row];
-            double Rv, Cv[6];
-            const double xi = jr[6 + 6 * row + x], xj = jr[18 + 6 * row + x];
-            if (dg) {
-              Rv = (ia ? xi : 0.0) - (ja ? xj : 0.0);
-#pragma unroll
-              for (int z = 0; z < 6; z++)
-                Cv[z] = (ia ? (double)jr[6 + 6 * row + z] : 0.0) - (ja ? (double)jr[18 + 6 * row + z] : 0.0);
-              acc[k][6] -= (wr * (double)jr[2 + row]) * Rv;
-            } else {
-              Rv = ia ? xi : xj;
-#pragma unroll
-              for (int z = 0; z < 6; z++)
-                Cv[z] = ia ? (double)jr[18 + 6 * row + z] : (double)jr[6 + 6 * row + z];
-            }
-            const double t = (dg ? wr : -wr) * Rv;
-#pragma unroll
-            for (int z = 0; z < 6; z++) acc[k][z] += t * Cv[z];
-          }
-        }
-        for (int r = pa; r < pb; r++) {
-          const unsigned m = D.pmask[r];
-          if (!((m >> ua) & 1u) || !((m >> ub) & 1u)) continue;
-          const int sa = D.soff[r] + __popc(m & ((1u << ua) - 1u));
-          const int sb = D.soff[r] + __popc(m & ((1u << ub) - 1u));
-          const double2 qu = D.qu[r];
-          const double qa = qu.x * D.Ev[6 * sa + x];
-          const double* eb = D.Ev + 6 * sb;
-#pragma unroll
-          for (int z = 0; z < 6; z++) acc[k][z] -= qa * eb[z];
-          if (dg) acc[k][6] -= (qu.x * qu.y) * D.Ev[6 * sa + x];
-        }
-      }
-      __syncthreads();
-      if (it == 0 && pa == 0) mark(A, 58);
-      if (it == 0 && A.marks && g == 0 && tid == 0) A.marks[59]++;  // passes
-      pa = pb;
-    }
-    if (it == 0 && A.marks && g == 0 && tid == 0) {
-      A.marks[60] = D.ne;
-      A.marks[61] = D.np;
-    }
-    mark(A, mb + 4);
-    if (A.marks && tid == 0 && it == 0 && g < 256) A.marks[1408 + g] = (int64_t)wall_clock64();
-    if (NB == 0) continue;  // structure only: dZ = Q u, applied after the loop
-    // ---- publish this workgroup's contribution (granules) ----
-    {
-      v4u* gout = A.gran + ((size_t)par * G + g) * rowg;
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc(gout, 0, 16 * rowg, kBufDword3);
-#pragma unroll
-      for (int k = 0; k < kDItems; k++) {
-        const int item = tid + k * kWT;
-        if (item >= NB * 6) continue;
-        const int blk = item / 6, x = item % 6;
-        const bool dg = (L.tri[blk] >> 8) == (L.tri[blk] & 0xff);
-        const int base = 16 * (blk * kDRow);
-        if (dg) {  // 21 lower entries + y (the block kernel's partial layout)
-#pragma unroll
-          for (int z = 0; z < 6; z++)
-            if (z <= x)
-              __builtin_amdgcn_raw_buffer_store_b128(granule(acc[k][z], gtag), rs,
-                                                     base + 16 * (x * (x + 1) / 2 + z), 0, kSc1);
-          __builtin_amdgcn_raw_buffer_store_b128(granule(acc[k][6], gtag), rs,
-                                                 base + 16 * (21 + x), 0, kSc1);
-        } else {
-#pragma unroll
-          for (int z = 0; z < 6; z++)
-            __builtin_amdgcn_raw_buffer_store_b128(granule(acc[k][z], gtag), rs,
-                                                   base + 16 * (6 * x + z), 0, kSc1);
-        }
-      }
-    }
-    mark(A, mb + 0);
-    if (A.marks && tid == 0 && it < 2 && g < 256) A.marks[128 + 256 * it + g] = (int64_t)wall_clock64();
-    // poll helper: T granules at byte offsets off(t) of buffer rs, values to dst(t)
-    auto poll = [&](__amdgpu_buffer_rsrc_t rs, int T, auto off_of, auto dst_of) {
-      constexpr int kIn = 16;
-      const long long tw0 = (long long)wall_clock64();
-      bool late = false;
-      for (int t0_ = tid; t0_ < T; t0_ += kIn * kWT) {
-        int off[kIn];
-        unsigned pend = 0;
-#pragma unroll
-        for (int r = 0; r < kIn; r++) {
-          const int t = min(t0_ + r * kWT, T - 1);
-          off[r] = off_of(t);
-          pend |= (t0_ + r * kWT < T) ? (1u << r) : 0u;
-        }
-        while (pend) {
-          v4u v[kIn];
-#pragma unroll
-          for (int r = 0; r < kIn; r++)
-            v[r] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(rs, off[r], 0, kSc1));
-#pragma unroll
-          for (int r = 0; r < kIn; r++) {
-            const bool ok = ((pend >> r) & 1u) && v[r].w == gtag && v[r].z == gran_hash(v[r].x, v[r].y);
-            if (ok) {
-              *dst_of(t0_ + r * kWT) =
-                  __longlong_as_double((long long)(((unsigned long long)v[r].y << 32) | v[r].x));
-              pend &= ~(1u << r);
-            }
-          }
-          if (!pend) break;
-          if ((long long)wall_clock64() - tw0 > kSpin) {
-            late = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      if (late) ctl[cTimeout] = 1;
-    };
-    // ---- reduce: workgroup b < NB sums block b over all workgroups ----
-    if (g < NB) {
-      const int blk = g;
-      const bool dg = (L.tri[blk] >> 8) == (L.tri[blk] & 0xff);
-      const int nk = dg ? 27 : 36;
-      double* stg = R;  // [G][kDRow]
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          A.gran + (size_t)par * G * rowg, 0, (int)(16 * (size_t)G * rowg), kBufDword3);
-      poll(rs, G * nk,
-           [&](int t) { return 16 * ((t / nk) * rowg + blk * kDRow + t % nk); },
-           [&](int t) { return stg + (t / nk) * kDRow + t % nk; });
-      __syncthreads();
-      v4u* rout = A.gran2 + (size_t)par * NB * kDRow + (size_t)blk * kDRow;
-      const __amdgpu_buffer_rsrc_t ro =
-          __builtin_amdgcn_make_buffer_rsrc(rout, 0, 16 * kDRow, kBufDword3);
-      for (int k = tid; k < nk; k += kWT) {
-        double s = 0.0;
-        for (int w = 0; w < G; w++) s += stg[w * kDRow + k];
-        if (dg && k < 21) {
-          int x = 0;
-          while ((x + 1) * (x + 2) / 2 <= k) x++;
-          if (k - x * (x + 1) / 2 == x) s += 1e-4 * s + 1.0;  // S += I (1e-4 S + 1) (:560)
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(granule(s, gtag), ro, 16 * k, 0, kSc1);
-      }
-    }
-    // ---- gather every reduced block, solve redundantly ----
-    double* Sd = R;
-    double* yd = Sd + 36 * NB;
-    double* tmpb = yd + 6 * N;  // [NB][kDRow] reduced values as gathered
-    __syncthreads();
-    {
-      const int T = N * 27 + (NB - N) * 36;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          A.gran2 + (size_t)par * NB * kDRow, 0, (int)(16 * (size_t)NB * kDRow), kBufDword3);
-      // flat index t -> (block, k): diagonal blocks first in lblk order?  No:
-      // blocks are in lblk order with 27 (diagonal) or 36 values; a prefix
-      // over that order is kept in LDS (bstart)
-      int* bstart = reinterpret_cast<int*>(tmpb + (size_t)NB * kDRow);
-      if (tid == 0) {
-        int s = 0;
-        for (int b = 0; b < NB; b++) {
-          bstart[b] = s;
-          s += ((L.tri[b] >> 8) == (L.tri[b] & 0xff)) ? 27 : 36;
-        }
-        bstart[NB] = s;
-      }
-      __syncthreads();
-      auto blk_of = [&](int t) {
-        int lo = 0, hi = NB - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (bstart[mid] <= t) lo = mid; else hi = mid - 1;
-        }
-        return lo;
-      };
-      poll(rs, T, [&](int t) { const int b = blk_of(t); return 16 * (b * kDRow + t - bstart[b]); },
-           [&](int t) { const int b = blk_of(t); return tmpb + b * kDRow + (t - bstart[b]); });
-    }
-    __syncthreads();
-    mark(A, mb + 1);
-    if (A.marks && tid == 0 && it < 2 && g < 256) A.marks[640 + 256 * it + g] = (int64_t)wall_clock64();
-    for (int t = tid; t < 36 * NB; t += kWT) {
-      const int blk = t / 36, k = t % 36;
-      const bool dg = (L.tri[blk] >> 8) == (L.tri[blk] & 0xff);
-      double s;
-      if (dg) {  // diagonal: 21 lower entries stored; mirror
-        const int x = k / 6, z = k % 6;
-        const int xx = x >= z ? x : z, zz = x >= z ? z : x;
-        s = tmpb[blk * kDRow + xx * (xx + 1) / 2 + zz];
-      } else {
-        s = tmpb[blk * kDRow + k];
-      }
-      Sd[t] = s;
-    }
-    for (int t = tid; t < 6 * N; t += kWT) {
-      const int i = t / 6, x = t % 6;
-      yd[t] = tmpb[lblk(i, i) * kDRow + 21 + x];
-    }
-    __syncthreads();
-    mark(A, mb + 2);
-    WSolve sv;
-    sv.S = Sd;
-    sv.y = yd;
-    sv.x = yd + 6 * N;
-    sv.r = sv.x + 6 * N;
-    sv.A = reinterpret_cast<float*>(sv.r + 6 * N);
-    sv.Z = sv.A + 36 * NB;
-    sv.v0 = sv.Z + 36 * NB;
-    sv.v1 = sv.v0 + 6 * N;
-    const bool ok = wsolve(sv, N, kRefine, &ctl[cFail]);
-    const bool zero = !ok || ctl[cTimeout] != 0;
-    for (int k = tid; k < 6 * N; k += kWT) {
-      const double v = zero ? 0.0 : sv.x[k];  // (dpvo/ba.py:17-21)
-      L.dX[k] = v;
-      if (g == 0 && A.dxo) A.dxo[k] = v;
-    }
-    if (!ok && tid == 0) ctl[cFailAny] = 1;
-    __syncthreads();
-    mark(A, mb + 3);
-  }
-
-  // ---------------- final apply + write-back ----------------
-  if (A.iters > 0) {
-    const int it = A.iters;
-    for (int i = tid; i < N; i += kWT) {
-      float xi[6], tt[3], qq[4], t1[3], q1[4];
-#pragma unroll
-      for (int k = 0; k < 6; k++) xi[k] = (float)L.dX[6 * i + k];
-      float* pl = L.pose + 8 * i;
-      tt[0] = pl[0]; tt[1] = pl[1]; tt[2] = pl[2];
-      qq[0] = pl[3]; qq[1] = pl[4]; qq[2] = pl[5]; qq[3] = pl[6];
-      retrSE3(xi, tt, qq, t1, q1);
-      pl[0] = t1[0]; pl[1] = t1[1]; pl[2] = t1[2];
-      pl[3] = q1[0]; pl[4] = q1[1]; pl[5] = q1[2]; pl[6] = q1[3];
-    }
-    for (int r = tid; r < D.np; r += kWT) {
-      const unsigned m = D.pmask[r];
-      double ex = 0.0;
-      int s = D.soff[r];
-      for (unsigned mm = (NB > 0 ? m : 0u); mm; mm &= mm - 1, s++) {
-        const int p = __builtin_ctz(mm);
-        const double* e = D.Ev + 6 * s;
-        const double* d = L.dX + 6 * p;
-        ex += e[0] * d[0] + e[1] * d[1] + e[2] * d[2] + e[3] * d[3] + e[4] * d[4] + e[5] * d[5];
-      }
-      const double2 qu = D.qu[r];
-      const float dz = (float)(qu.x * (qu.y - ex));
-      const float base = (it == 1) ? D.dbase[r] : D.dep[r];
-      float d = base + dz;
-      d = (d > 20.0f) ? 1.0f : d;
-      D.dep[r] = (float)fmax((double)d, 1e-4);
-    }
-    __syncthreads();
-    for (int k = tid; k < D.np * PP; k += kWT) {
-      const int r = k / PP, c = k % PP;
-      A.patches[(size_t)D.pkx[r] * 3 * PP + 2 * PP + c] = D.dep[r];
-    }
-    if (g == 0)
-      for (int i = tid; i < N; i += kWT) {
-        const int gp = t0w + i;
-        if (gp >= 0 && gp < A.num_poses)
-          for (int c = 0; c < 7; c++) A.poses[7 * (size_t)gp + c] = L.pose[8 * i + c];
-      }
-  }
-  if (tid == 0) {
-    int st = 0;
-    if (ctl[cTimeout]) st |= kStTimeout;
-    if (g == 0) st |= A.plan.meta[2];  // kk clamp from the plan
-    if (ctl[cCap]) st |= kStCap;
-    if (g == 0 && ctl[cFailAny]) st |= kStChol;
-    if (st) {
-      atomicOr(A.status, st);
-      if (A.sink) atomicOr(A.sink, st);
-    }
-    if (g == 0) {
-      __hip_atomic_store(&A.flags[kEpochWord], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      mark(A, 63);
-    }
-  }
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------- host side
@@ -2549,27 +1911,10 @@ static size_t al256w(size_t v) { return (v + 255) / 256 * 256; }
 
 struct WGrid {
   int NB, Sd, So, G;
-  bool dense;  // ba_dense_kernel (patch-partitioned) instead of ba_window_kernel
 };
-// dense (patch-partitioned) kernel: DPVO-shaped windows, where a patch sees
-// most free poses (E > 2048: the block kernel re-linearises each edge for up
-// to N(N+1)/2 blocks); DPVO_BA_DENSE=0/1 overrides (A/B)
-static bool use_dense(int E) {
-  static const char* ov = getenv("DPVO_BA_DENSE");
-  if (ov && (ov[0] == '0' || ov[0] == '1')) return ov[0] == '1';
-  return false;
-}
 static WGrid window_grid(int E, int N) {
   WGrid w;
   w.NB = N * (N + 1) / 2;
-  w.dense = use_dense(E);
-  if (w.dense) {
-    // one workgroup per ~64 edges (own edges live in LDS), at least one per
-    // lower block (workgroup b reduces block b)
-    w.Sd = w.So = 1;
-    w.G = std::min(std::max(std::max(w.NB, (E + 63) / 64), 1), kWMaxG);
-    return w;
-  }
   if (N <= 0) {
     w.Sd = w.So = 1;
     w.G = 1;
@@ -2580,15 +1925,6 @@ static WGrid window_grid(int E, int N) {
   // every block alike, so large windows split all blocks evenly
   w.So = E > 2048 ? 4 : 1;
   w.Sd = 4;
-  // tuning override (instrumentation): DPVO_BA_SHARES="Sd,So"
-  static const char* ov = getenv("DPVO_BA_SHARES");
-  if (ov) {
-    int sd = 0, so = 0;
-    if (sscanf(ov, "%d,%d", &sd, &so) == 2 && sd >= 1 && so >= 1 && sd <= 16 && so <= 16) {
-      w.Sd = sd;
-      w.So = so;
-    }
-  }
   auto G = [&]() { return N * w.Sd + (w.NB - N) * w.So; };
   while (G() > kWMaxG && w.Sd > 1) {
     if (w.Sd > w.So) w.Sd--;
@@ -2610,21 +1946,35 @@ static int window_coresident() {
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find(dev);
   if (it != cache.end()) return it->second;
-  int cus = 0, per = 0, per_d = 0;
+  int cus = 0, per = 0;
   (void)hipFuncSetAttribute((const void*)ba_window_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
-  (void)hipFuncSetAttribute((const void*)ba_dense_kernel,
                             hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)ba_window_kernel, kWT,
-                                                   kWLds) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_d, (const void*)ba_dense_kernel, kWT,
                                                    kWLds) != hipSuccess) {
     (void)hipGetLastError();
-    cus = per = per_d = 0;
+    cus = per = 0;
   }
-  cache[dev] = cus * std::min(per, per_d);
+  cache[dev] = cus * per;
   return cache[dev];
+}
+
+// per-process granule-key salt (granule()): drawn once from the OS entropy
+// source, mixed with the clock and the pid in case the source is weak
+static unsigned long long granule_salt() {
+  static const unsigned long long salt = [] {
+    unsigned long long v = 0;
+    try {
+      std::random_device rd;
+      v = ((unsigned long long)rd() << 32) ^ rd();
+    } catch (...) {
+    }
+    v ^= (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count() *
+         0x9E3779B97F4A7C15ull;
+    v ^= (unsigned long long)getpid() << 17;
+    return v;
+  }();
+  return salt;
 }
 
 bool ba_window_supported(int E, int N, int P) {
@@ -2633,12 +1983,8 @@ bool ba_window_supported(int E, int N, int P) {
   return G <= kWMaxG && G <= window_coresident();
 }
 
-// granules of one grid: block kernel [2][G][kGranPad]; dense kernel
-// [2][G][NB * 36] contributions + [2][NB][36] reduced blocks
-static size_t gran_count(const WGrid& w) {
-  return w.dense ? (size_t)2 * w.G * w.NB * kDRow + (size_t)2 * w.NB * kDRow
-                 : (size_t)2 * kGranPad * w.G;
-}
+// granules of one grid: [2][G][kGranPad]
+static size_t gran_count(const WGrid& w) { return (size_t)2 * kGranPad * w.G; }
 
 size_t ba_window_scratch_bytes(int E, int N) {
   const WGrid w = window_grid(E, N);
@@ -2716,8 +2062,6 @@ static void set_attrs() {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)ba_window_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
-    (void)hipFuncSetAttribute((const void*)ba_dense_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
     (void)hipFuncSetAttribute((const void*)ba_plan_kernel,
                               hipFuncAttributeMaxDynamicSharedMemorySize, kWLds);
@@ -2875,7 +2219,6 @@ int ba_window_run(float* poses, float* patches, const float* intrinsics, const f
   a.part = (double*)s;
   s += al256w(sizeof(double) * 2 * kPartPad * (size_t)w.G);
   a.gran = (v4u*)s;
-  a.gran2 = w.dense ? a.gran + (size_t)2 * w.G * w.NB * kDRow : nullptr;
   s += al256w((size_t)16 * gran_count(w));
   a.ejg = (float*)s;
   a.poses = poses;
@@ -2903,10 +2246,8 @@ int ba_window_run(float* poses, float* patches, const float* intrinsics, const f
   a.sink = a.plan.sink;
   a.marks = marks;
   a.dxo = dxo;
-  if (w.dense)
-    hipLaunchKernelGGL(ba_dense_kernel, dim3(w.G), dim3(kWT), kWLds, st, a);
-  else
-    hipLaunchKernelGGL(ba_window_kernel, dim3(w.G), dim3(kWT), kWLds, st, a);
+  a.salt = granule_salt();
+  hipLaunchKernelGGL(ba_window_kernel, dim3(w.G), dim3(kWT), kWLds, st, a);
   return launch_status();
 }
 

@@ -24,6 +24,10 @@
 
 // diagnostic builds (scripts/micro/corr_bench.hip) define CORR_STAMP(slot) to
 // record per-wave shader-clock stamps; the library compiles it away
+#ifndef CORR_TSTAMP  // per-tile stamps (diagnostic builds): tile i, point k
+#define CORR_TSTAMP(i, k)
+#define CORR_TSTAMP_INIT
+#endif
 #ifndef CORR_STAMP
 #define CORR_STAMP(slot)
 #define CORR_STAMP_RT(slot)
@@ -39,10 +43,10 @@ constexpr int kBoxStride = 16 * kMaxTiles + 4;  // +4: the 4 row groups of a G t
 constexpr int kMaxL = 4;        // levels per launch
 constexpr int kOutPerLane = 8;  // (2R+1)^2 * p*p <= 512 outputs per level
 constexpr int kNpMax = 16;      // p*p <= 16 (one MFMA row tile)
-// Box tiles per wave in the register ring (kRing - 1 in flight).  Measured
-// (scripts/micro/corr_bench, cfg2 shape): 3, 4 and 5 run within 3 % of each
-// other -- past the first level the loop is bound by the f32 MFMA issue rate,
-// not by load latency -- so the shallowest ring (fewest VGPRs) is kept.
+// Box tiles per wave in the register ring (kRing - 1 in flight).  A 4-deep
+// ring (two waves per SIMD, al' fragments in LDS to fit 256 VGPRs) measured
+// 55.7 us against 53.9 for 3 (scripts/micro/corr_bench, cfg2 shape), and
+// round 4's deeper rings at one wave per SIMD were no faster either.
 constexpr int kRing = 3;
 
 struct NhwcLevels {
@@ -62,11 +66,38 @@ struct NhwcGeom {
   int xlo, ylo, bw, bh, ntile, pad[3];  // the level's (wave-uniform) box
 };
 
+// Box tiles of flattened position j (level level_at(j)) of a wave's edge, in
+// LDS: the per-tile load address is one broadcast LDS read plus a few VALU
+// ops (selecting among per-level registers by a run-time position compiled
+// to chains of scalar branches: ~80 SALU instructions per tile)
+struct alignas(16) TileDesc {
+  const void* base;  // box origin (frame, level)
+  int row, bw;       // elements per map row (W2 * C), box width
+  int npx;           // box pixels
+  float rbw;         // 1 / bw
+  int c0, c1;        // flattened tile range [c0, c1) of the position
+  int lvl, pad[3];
+};
+
+// LDS bytes of one corr_nhwc_kernel workgroup: per wave G, the level
+// geometry, the output block and the tile descriptors
+inline size_t corr_nhwc_lds_bytes(int np, int R, int L) {
+  return sizeof(float) * kNhwcWaves * np * kBoxStride + sizeof(NhwcGeom) * kNhwcWaves * kMaxL +
+         sizeof(float) * kNhwcWaves * corr_obuf_floats(np, R, L) +
+         sizeof(TileDesc) * kNhwcWaves * kMaxL + 16 * 4 * kWave * kNhwcWaves;
+}
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // 16-B tile vector (a native
-                                                                  // vector: a uint4 struct copy is a
-                                                                  // memcpy that keeps the ring in scratch)
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+// 16-B tile vector (a native vector: a uint4 struct copy is a memcpy that
+// keeps the ring in scratch)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// global-address-space view of a tile vector: the box base comes out of LDS
+// (TileDesc), where the compiler loses the pointer's address space -- a
+// generic pointer makes every tile load a flat load, which counts in both
+// vmcnt and lgkmcnt and makes the wait before each tile drain the whole ring
+typedef const __attribute__((address_space(1))) u32x4 gu32x4;
 
 // fp16 features (DPVO's MIXED_PRECISION runtime, correlation_kernel.py:552-654):
 // v_mfma_f32_16x16x16_f16, fp32 accumulation (documented deviation: the
@@ -137,6 +168,9 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   float* obuf = reinterpret_cast<float*>(reinterpret_cast<NhwcGeom*>(smem + kNhwcWaves * np * kBoxStride) +
                                          kNhwcWaves * kMaxL);
   obuf += wid * ostride;
+  // tile descriptors after the output blocks of all waves
+  TileDesc* td = reinterpret_cast<TileDesc*>(obuf - wid * ostride + kNhwcWaves * ostride) +
+                 wid * kMaxL;
   int edge;
   if (order) {
     // XCD-aware: workgroups are dispatched round-robin over the 8 XCDs, so
@@ -153,6 +187,7 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     if (edge >= B * M) return;  // waves are independent: no block barrier below
   }
   const int b = edge / M, m = edge % M;
+  CORR_TSTAMP_INIT;
   CORR_STAMP(0);
   CORR_STAMP_RT(12);
   CORR_STAMP_ID(14);
@@ -167,7 +202,15 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   // c = 16h + 4q + s at K step 4h + s (the same channel order as the B loads)
   const int ai = lane & 15, aq = lane >> 4;
   constexpr bool kHalf = std::is_same<T, __half>::value;
-  float Af[kHalf ? 1 : kNhwcC / 4];
+  // fp32 features: split-f16 A fragments (see mma below).  K step t of a
+  // v_mfma_f32_16x16x32_f16 takes, for lane (i, q), the 8 channels
+  // 16 (2t) + 4q + {0..3} and 16 (2t + 1) + 4q + {0..3} of patch pixel i --
+  // the channels of the lane's B loads B[2t], B[2t + 1] of a tile.
+  //   a = (Ah + Al 2^-11) 2^ae     (ae != 0 only if the patch holds |a| >= 2^14)
+  f16x8 Ah[kHalf ? 1 : 4];
+  // the al' fragments [t][lane] in LDS (read once per K step of a tile)
+  f16x8* Alds = reinterpret_cast<f16x8*>(td + kNhwcWaves * kMaxL - wid * kMaxL) + wid * 4 * kWave;
+  float ainv = 1.0f;  // 2^ae: multiplies the tile sums
   f16x4 Afh[kHalf ? kNhwcC / 16 : 1];
   // the patch's loads are issued here; they are staged into the A fragments
   // only after the first box tiles have been issued (build_A below), so the
@@ -203,11 +246,32 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
                            : (_Float16)0.0f;
         }
     } else {
+      float a[kNhwcC / 4];  // a[8t + j]: K step t, element j (channel 16 (2t + j/4) + 4q + j%4)
 #pragma unroll
       for (int h = 0; h < kNhwcC / 16; h++)
 #pragma unroll
-        for (int s = 0; s < 4; s++)
-          Af[4 * h + s] = arow ? G[(16 * h + 4 * aq + s) * np + ai] : 0.0f;
+        for (int s = 0; s < 4; s++) a[4 * h + s] = arow ? G[(16 * h + 4 * aq + s) * np + ai] : 0.0f;
+      // patch magnitude (wave max of |a| as bits: non-negative floats order
+      // like ints): a patch with |a| >= 2^14 is scaled by an exact power of
+      // two so its f16 pieces cannot overflow; the tile sums are scaled back
+      int mb = 0;
+#pragma unroll
+      for (int k = 0; k < kNhwcC / 4; k++) mb = max(mb, (int)(__float_as_uint(a[k]) & 0x7fffffffu));
+      mb = wave_max_i(mb);
+      const int ae = (mb >= 0x46800000 && mb < 0x7f800000) ? ((mb >> 23) - 127) - 13 : 0;
+      const float asc = __uint_as_float((unsigned)(127 - ae) << 23);
+      ainv = __uint_as_float((unsigned)(127 + ae) << 23);
+      f16x8 al;
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const float v = a[8 * t + j] * asc;
+          const _Float16 hv = (_Float16)v;
+          Ah[t][j] = hv;
+          al[j] = (_Float16)((v - (float)hv) * 2048.0f);
+          if (j == 7) Alds[t * kWave + lane] = al;
+        }
     }
     wave_lds_sync();  // A fragments read: G free again
   };
@@ -390,59 +454,60 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   const int nT = cum[kMaxL];  // == cum[L]: positions >= L add no tiles
   constexpr int V = CorrT<T>::kVecs;  // 16-B loads per lane per tile
   // Per flattened position j (level level_at(j)): the box origin pointer, the
-  // box row stride, width, pixel count and 1 / width, materialised once in
-  // registers so the per-tile address math is a few selects on registers (no
-  // branches, no kernel-argument or LDS reads, no division per tile).
-  const T* pbase[kMaxL];
-  int prow[kMaxL], pbw[kMaxL], pnpx[kMaxL];
-  float prbw[kMaxL];
-#pragma unroll
-  for (int j = 0; j < kMaxL; j++) {
+  // box row stride, width, pixel count and 1 / width and the position's tile
+  // range, one TileDesc per position in LDS (lane j writes entry j)
+  if (lane < kMaxL) {
+    const int j = lane;
     const int l = (j < L) ? level_at(j) : 0;
     const NhwcGeom* gg = geo + l;
     const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
-    const int bw0 = max(wave_uniform(gg->bw), 1);
-    pbw[j] = bw0;
-    pnpx[j] = bw0 * wave_uniform(gg->bh);
-    prbw[j] = 1.0f / (float)bw0;
-    prow[j] = W2 * C;
+    const int gbw = gg->bw, gbh = gg->bh;
+    const int bw0 = max(gbw, 1);
     // an empty box reads the frame's first pixel (in range whatever the
     // coordinates): the ring preload below is then unconditional
-    const bool empty = wave_uniform(gg->bw) <= 0 || wave_uniform(gg->bh) <= 0;
-    pbase[j] = static_cast<const T*>(LV_SEL(f2, l)) +
-               (((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 +
-                (empty ? 0 : (size_t)wave_uniform(gg->ylo) * W2 + wave_uniform(gg->xlo))) * C;
+    const bool empty = gbw <= 0 || gbh <= 0;
+    TileDesc d;
+    d.base = static_cast<const T*>(LV_SEL(f2, l)) +
+             (((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 +
+              (empty ? 0 : (size_t)gg->ylo * W2 + gg->xlo)) * C;
+    d.row = W2 * C;
+    d.bw = bw0;
+    d.npx = bw0 * gbh;
+    d.rbw = 1.0f / (float)bw0;
+    d.c0 = j == 0 ? cum[0] : j == 1 ? cum[1] : j == 2 ? cum[2] : cum[3];
+    d.c1 = j == 0 ? cum[1] : j == 1 ? cum[2] : j == 2 ? cum[3] : cum[4];
+    d.lvl = l;
+    d.pad[0] = d.pad[1] = d.pad[2] = 0;
+    td[j] = d;
   }
-  auto pick = [](int j, auto a0, auto a1, auto a2, auto a3) __attribute__((always_inline)) {
-    return j == 0 ? a0 : j == 1 ? a1 : j == 2 ? a2 : a3;
+  wave_lds_sync();
+  auto pos_of = [&](int i) __attribute__((always_inline)) {  // flattened tile -> position
+    return (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
   };
   // Tile i's loads: lane (i, q) reads 16 B of box pixel i directly in the MFMA
   // B layout (16 pixels x 64 B per instruction).  (Whole-line loads staged
   // through an LDS image and read back as B fragments measured 5-8 % slower.)
   auto load_tile = [&](u32x4 (&dst)[V], int i) __attribute__((always_inline)) {
     i = min(i, max(nT - 1, 0));  // past the end: re-read the last tile (never used)
-    const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
-    const int t = i - pick(j, 0, cum[1], cum[2], cum[3]);
-    const T* base = pick(j, pbase[0], pbase[1], pbase[2], pbase[3]);
-    const int row = pick(j, prow[0], prow[1], prow[2], prow[3]);
-    const int bw0 = pick(j, pbw[0], pbw[1], pbw[2], pbw[3]);
-    const int npx = pick(j, pnpx[0], pnpx[1], pnpx[2], pnpx[3]);
-    const float rbw = pick(j, prbw[0], prbw[1], prbw[2], prbw[3]);
+    const TileDesc d = td[pos_of(i)];
+    const int t = i - d.c0;
     auto pix = [&](int q) __attribute__((always_inline)) -> int {  // element offset of box pixel 16t + q
-      const int px = min(16 * t + q, max(npx - 1, 0));  // pad columns read pixel npx-1
-      const int r = (int)(((float)px + 0.5f) * rbw), cc = px - r * bw0;
-      return r * row + cc * C;
+      const int px = min(16 * t + q, max(d.npx - 1, 0));  // pad columns read pixel npx-1
+      const int r = (int)(((float)px + 0.5f) * d.rbw), cc = px - r * d.bw;
+      return r * d.row + cc * C;
     };
     {
-      const T* s = base + pix(ai) + CorrT<T>::kLaneCh * aq;
+      const T* s = static_cast<const T*>(d.base) + pix(ai) + CorrT<T>::kLaneCh * aq;
 #pragma unroll
       for (int h = 0; h < V; h++)
 #if defined(CORR_DIAG_NO_LOAD)  // diagnostic builds only: no tile loads
         dst[h] = (u32x4){(unsigned)h, (unsigned)i, 0u, 0u};
 #elif defined(CORR_NT_LOADS)  // diagnostic builds: streaming (non-temporal) tile loads
-        dst[h] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s + (kHalf ? 8 * h : 16 * h)));
+        dst[h] = __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(
+            reinterpret_cast<uintptr_t>(s + (kHalf ? 8 * h : 16 * h))));
 #else
-        dst[h] = *reinterpret_cast<const u32x4*>(s + (kHalf ? 8 * h : 16 * h));
+        dst[h] = *reinterpret_cast<const gu32x4*>(
+            reinterpret_cast<uintptr_t>(s + (kHalf ? 8 * h : 16 * h)));
 #endif
     }
   };
@@ -462,61 +527,108 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     __builtin_amdgcn_sched_barrier(0);
   }
   build_A();
+  // Level l the scalar way: raw[k][yy][xx] as fp32 dot products straight
+  // from HBM into G, then the bilinear.  Levels off the fast path (windows too
+  // spread for it), and fast-path levels with a non-finite tile (split-f16
+  // products: |feature| >= 65520, or infinite / NaN features).
+  auto raw_level = [&](int l) {
+    const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
+    const T* f2 = static_cast<const T*>(LV_SEL(f2, l)) + ((size_t)b * N2 + jx) * H2 * W2 * C;
+    wave_lds_sync();  // G's tiles (if any) read
+    for (int e = lane; e < np * D * D; e += kWave) {
+      const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
+      const int i1 = geo[l].y0[k] + yy - R, j1 = geo[l].x0[k] + xx - R;
+      float sacc = 0.f;
+      if (idx_ok && i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
+        const T* px = f2 + ((size_t)i1 * W2 + j1) * C;
+        const T* f1 = fmap1 + ((size_t)b * N1 + ix) * C * np;
+        for (int c = 0; c < C; c++) sacc += to_acc(f1[(size_t)c * np + k]) * to_acc(px[c]);
+      }
+      G[e] = sacc;
+    }
+    wave_lds_sync();
+    bilinear(l, false);
+    wave_lds_sync();
+  };
   // levels off the fast path (empty box, or windows too spread for it) first
   for (int l = 0; l < L; l++) {
     const int nt = wave_uniform(geo[l].ntile);
-    if (nt > kMaxTiles) {  // raw[k][yy][xx] directly into G
-      const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
-      const T* f2 = static_cast<const T*>(LV_SEL(f2, l)) + ((size_t)b * N2 + jx) * H2 * W2 * C;
-      for (int e = lane; e < np * D * D; e += kWave) {
-        const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
-        const int i1 = geo[l].y0[k] + yy - R, j1 = geo[l].x0[k] + xx - R;
-        float sacc = 0.f;
-        if (idx_ok && i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
-          const T* px = f2 + ((size_t)i1 * W2 + j1) * C;
-          const T* f1 = fmap1 + ((size_t)b * N1 + ix) * C * np;
-          for (int c = 0; c < C; c++) sacc += to_acc(f1[(size_t)c * np + k]) * to_acc(px[c]);
-        }
-        G[e] = sacc;
-      }
-      wave_lds_sync();
-      bilinear(l, false);
-      wave_lds_sync();
+    if (nt > kMaxTiles) {
+      raw_level(l);
     } else if (nt == 0) {
       bilinear(l, true);  // every tap reads 0 (out of the empty box)
     }
   }
 
   if (nT > 0) {
+    bool bad = false;  // a non-finite split-f16 tile in the current level
+    // Deferred G store: tile i's sums are written in step i + 1, after that
+    // step's MFMAs are issued, so the wave never stalls on the chain it has
+    // just issued (a level's last tile is stored at once, before the bilinear)
+    f32x4 pg0 = {0.f, 0.f, 0.f, 0.f}, pg1 = {0.f, 0.f, 0.f, 0.f};
+    int pgoff = -1;  // G column of the pending tile (16 t), -1: none
+    auto store_g = [&](const f32x4& a0, const f32x4& a1, int toff) __attribute__((always_inline)) {
+      // D: lane holds rows 4q + r (patch pixels), column lane & 15 (box pixel)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = 4 * aq + r;
+        if (row < np) {
+          if constexpr (kHalf) G[row * kBoxStride + toff + ai] = a0[r] + a1[r];
+          else G[row * kBoxStride + toff + ai] = (a0[r] + a1[r] * (1.0f / 2048.0f)) * ainv;
+        }
+      }
+    };
     auto step = [&](u32x4 (&cur)[V], int i) __attribute__((always_inline)) {
       const bool live = i < nT;  // the last group may hold 1-2 slots past the end
-      // two accumulators (even / odd channel groups): two independent MFMA
-      // chains, summed once per tile in a fixed order
+      // the tile's G values: fp16 acc0 + acc1; fp32 (acc0 + acc1 2^-11) 2^ae
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
       auto mma = [&](const u32x4 (&B)[V]) __attribute__((always_inline)) {
         if constexpr (kHalf) {
-          // 8 K steps of 16 channels: vector h holds steps 2h (lo) and 2h + 1 (hi)
+          // 4 K steps of 32 channels: vector h holds the lane's channels
+          // 32q + 8h .. + 7, A the same channels (Afh[2h], Afh[2h + 1])
 #pragma unroll
           for (int h = 0; h < V; h++) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x16f16(Afh[2 * h], h4_lo(B[h]), acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x16f16(Afh[2 * h + 1], h4_hi(B[h]), acc1, 0, 0, 0);
+            const f16x8 a8 = __builtin_shufflevector(Afh[2 * h], Afh[2 * h + 1], 0, 1, 2, 3, 4, 5,
+                                                     6, 7);
+            const f16x8 b8 = __builtin_bit_cast(f16x8, B[h]);
+            if (h & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8, b8, acc1, 0, 0, 0);
+            else acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8, b8, acc0, 0, 0, 0);
           }
         } else {
+          // fp32 features, split-f16 products (VERDICT r04 item 3 option 2):
+          // b = bh + bl with bh = f16(b), bl = f16(b - bh) (RNE), and per edge
+          // a = (ah + al' 2^-11) 2^ae (al' = f16((a - ah) 2^11), build_A);
+          //   a b 2^-ae = ah bh + ah bl + (al' bh) 2^-11   (+ al bl, dropped)
+          // Each f16 x f16 product is exact in fp32 and v_mfma_f32_16x16x32_f16
+          // accumulates in fp32: per product |err| <= 2^-21 |a||b| + 2^-25 |a|
+          // (bl below the f16 normal range for |b| < 2^-3), against 2^-24
+          // per fp32 rounding.  12 MFMAs of 16 cycles per tile
+          // instead of 32 v_mfma_f32_16x16x4_f32 of 32.  |b| >= 65520 makes
+          // bh infinite: a tile whose sums come out non-finite is redone on
+          // the scalar fp32 path (raw_level), which also gives the fp32
+          // result for infinite / NaN features.
 #pragma unroll
-          for (int h = 0; h < 8; h += 2) {
-            const float4 c0 = __builtin_bit_cast(float4, B[h]);
-            const float4 c1 = __builtin_bit_cast(float4, B[h + 1]);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 0], c0.x, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 4], c1.x, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 1], c0.y, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 5], c1.y, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 2], c0.z, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 6], c1.z, acc1, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 3], c0.w, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 7], c1.w, acc1, 0, 0, 0);
+          for (int t = 0; t < 4; t++) {
+            const float4 c0 = __builtin_bit_cast(float4, B[2 * t]);
+            const float4 c1 = __builtin_bit_cast(float4, B[2 * t + 1]);
+            const float x[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+            f16x8 bh, bl;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+              const _Float16 hv = (_Float16)x[j];
+              bh[j] = hv;
+              bl[j] = (_Float16)(x[j] - (float)hv);
+            }
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah[t], bh, acc0, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah[t], bl, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Alds[t * kWave + lane], bh, acc1, 0, 0, 0);
           }
+          const bool fin = __builtin_isfinite(acc0[0] + acc0[1] + acc0[2] + acc0[3] + acc1[0] +
+                                              acc1[1] + acc1[2] + acc1[3]);
+          bad = bad || __builtin_amdgcn_ballot_w64(!fin) != 0;
         }
       };
+      CORR_TSTAMP(i, 0);
 #ifndef CORR_DIAG_NO_MMA  // diagnostic builds only (timing of the rest of the tile loop)
       if (live) mma(cur);
 #else
@@ -525,27 +637,38 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
         acc1[0] = __builtin_bit_cast(float, cur[V - 1].w);
       }
 #endif
+      if (pgoff >= 0) {  // the previous tile's sums (its MFMA chain has drained)
+        store_g(pg0, pg1, pgoff);
+        pgoff = -1;
+      }
       {
         // refill this slot with tile i + kRing (past the end: the last tile again,
         // never used); unconditional, so every path into the next group has the
         // same load order and the wait before a tile drains only that tile's loads
         load_tile(cur, i + kRing);
       }
+      CORR_TSTAMP(i, 1);
       if (!live) return;
-      const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
-      const int t = i - pick(j, 0, cum[1], cum[2], cum[3]), l = level_at(j);
-      // D: lane holds rows 4q + r (patch pixels), column lane & 15 (box pixel)
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int row = 4 * aq + r;
-        if (row < np) G[row * kBoxStride + 16 * t + ai] = acc0[r] + acc1[r];
+      const TileDesc& d = td[pos_of(i)];
+      const int t = i - d.c0, l = wave_uniform(d.lvl);
+      const bool lend = i + 1 == wave_uniform(d.c1);
+      if (!lend) {
+        pg0 = acc0;
+        pg1 = acc1;
+        pgoff = wave_uniform(16 * t);
       }
-      const int le = pick(j, cum[1], cum[2], cum[3], cum[4]);
-      if (i + 1 == le) {  // level complete: bilinear, then G is free again
-        wave_lds_sync();
+      CORR_TSTAMP(i, 2);
+      if (lend) {  // level complete: its last sums, the bilinear, then G is free again
+        store_g(acc0, acc1, 16 * t);
         CORR_STAMP(2 + 2 * l);
-        bilinear(l, true);
-        wave_lds_sync();
+        if (bad) {  // rare: redo the level on the scalar fp32 path
+          raw_level(l);
+          bad = false;
+        } else {
+          wave_lds_sync();
+          bilinear(l, true);
+          wave_lds_sync();
+        }
         CORR_STAMP(3 + 2 * l);
       }
     };
@@ -569,323 +692,6 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   }
   CORR_STAMP(11);
   CORR_STAMP_RT(13);
-}
-
-// ---------------------------------------------------------------------------
-// Channel-split variant (fp32, p = 3, R = 3: DPVO's shape; EXPERIMENT, opt-in
-// with DPVO_CORR_SPLIT=1: it measured 88.8 us against the one-wave kernel's
-// 57.5 us at cfg2, see DESIGN.md §3 A-CORR round 4).  At cfg2 there are
-// 2048 edges = 2 waves per SIMD with one wave per edge, and inside a wave the
-// f32 MFMAs of a tile and the gathers of the next do not overlap well
-// (DESIGN.md §3 A-CORR diagnostics).  Here an edge is a 128-thread workgroup
-// of TWO waves, wave h owning channels [64h, 64h + 64): each wave runs half the
-// MFMAs (16 per tile) over half the bytes (4 x 16-B loads per lane per tile),
-// with half the ring registers, so the kernel fits 4 waves per SIMD and twice
-// as many independent tile streams hide each other's latency.  The two
-// partial G tiles meet in LDS through ds_add_f32 onto zero (0 + a + b rounds
-// the same in either order: deterministic); one LDS-only barrier pair per
-// level, the bilinear split by patch pixel k between the waves.
-// ---------------------------------------------------------------------------
-constexpr int kSplitThreads = 2 * kWave;
-constexpr int kSplitVecs = 4;  // 16-B loads per lane per tile (64 channels of a pixel)
-constexpr int kSplitRing = 3;
-
-__device__ __forceinline__ void wg_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-__global__ void __launch_bounds__(kSplitThreads, 4)  // 4 waves per SIMD (<= 128 VGPRs)
-    corr_split_kernel(const float* __restrict__ fmap1, NhwcLevels lv, int L,
-                      const float* __restrict__ coords, const int64_t* __restrict__ ii,
-                      const int64_t* __restrict__ jj, int B, int M, int N1, int N2,
-                      const int* __restrict__ order, float* __restrict__ out) {
-  constexpr int np = 9, R = 3, D = 2 * R + 2, Dp = D - 1, nout = Dp * Dp * np;
-  constexpr int C = kNhwcC, V = kSplitVecs;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int hw = wave_uniform(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
-  float* G = smem;                                                  // [np][kBoxStride]
-  NhwcGeom* geo = reinterpret_cast<NhwcGeom*>(G + np * kBoxStride) + hw * kMaxL;  // per wave
-  float* obuf = reinterpret_cast<float*>(reinterpret_cast<NhwcGeom*>(G + np * kBoxStride) +
-                                         2 * kMaxL);                // [nout][L]
-  int edge;
-  if (order) {  // XCD-aware, as corr_nhwc_kernel (one edge per workgroup)
-    const int per = (M + 7) / 8;
-    const int p = (blockIdx.x % 8) * per + blockIdx.x / 8;
-    if (p >= M) return;  // workgroup-uniform
-    edge = wave_uniform(order[p]);
-  } else {
-    edge = blockIdx.x;
-    if (edge >= B * M) return;
-  }
-  const int b = edge / M, m = edge % M;
-  const int ix = wave_uniform((int)ii[m]), jx = wave_uniform((int)jj[m]);
-  const bool idx_ok = ix >= 0 && ix < N1 && jx >= 0 && jx < N2;
-  const float cv = (lane < 2 * np) ? coords[((size_t)b * M + m) * 2 * np + lane] : 0.f;
-  __builtin_amdgcn_sched_barrier(0);
-
-  // this wave's half of the gmap patch: channels [64 hw, 64 hw + 64) x 9 =
-  // 144 16-B units, staged through the wave's own part of G (zeroed after)
-  const int ai = lane & 15, aq = lane >> 4;
-  constexpr int kUnits = 64 * np / 4, kRA = (kUnits + kWave - 1) / kWave;
-  u32x4 st[kRA];
-  {
-    const float* f1 = fmap1 + ((size_t)b * N1 + (idx_ok ? ix : 0)) * C * np + 64 * hw * np;
-#pragma unroll
-    for (int r = 0; r < kRA; r++)
-      st[r] = reinterpret_cast<const u32x4*>(f1)[min(lane + kWave * r, kUnits - 1)];
-  }
-  __builtin_amdgcn_sched_barrier(0);  // patch loads before the tile loads: their wait counts only them
-  float Af[16];  // A fragment of K step 4h + s: f1[64 hw + 16 h + 4 aq + s][ai]
-  float* stg = G + hw * (64 * np);
-  auto build_A = [&]() __attribute__((always_inline)) {
-    // unconditional: lanes past the end rewrite the last unit with its own
-    // value (a guarded store is a branch whose wait drains the tile loads)
-#pragma unroll
-    for (int r = 0; r < kRA; r++)
-      reinterpret_cast<u32x4*>(stg)[min(lane + kWave * r, kUnits - 1)] = st[r];
-    wave_lds_sync();
-    const bool arow = idx_ok && ai < np;
-#pragma unroll
-    for (int h = 0; h < 4; h++)
-#pragma unroll
-      for (int s = 0; s < 4; s++) Af[4 * h + s] = arow ? stg[(16 * h + 4 * aq + s) * np + ai] : 0.0f;
-  };
-
-  // geometry of every level (both waves, own copy: no barrier before the
-  // first tile loads)
-  int cum[kMaxL + 1];
-  {
-    const int gl = lane >> 4, gk = lane & 15;
-    const bool act = gl < L && gk < np;
-    const float xr = __shfl(cv, min(gk, np - 1), kWave), yr = __shfl(cv, np + min(gk, np - 1), kWave);
-    const float sc = LV_SEL(scale, gl < L ? gl : 0);
-    const bool pow2 = (__float_as_uint(sc) & 0x7fffffu) == 0u;
-    const float rs = 1.0f / sc;
-    const float x = pow2 ? xr * rs : xr / sc, y = pow2 ? yr * rs : yr / sc;
-    const int xf = ifloor_safe(x), yf = ifloor_safe(y);
-    if (act) {
-      geo[gl].x0[gk] = xf;
-      geo[gl].y0[gk] = yf;
-      geo[gl].dx[gk] = x - floorf(x);  // correlation_kernel.cu:262
-      geo[gl].dy[gk] = y - floorf(y);
-    }
-    int xlo = act ? xf : 0x7fffffff, ylo = act ? yf : 0x7fffffff;
-    int xhi = act ? xf : -0x7fffffff, yhi = act ? yf : -0x7fffffff;
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) {
-      xlo = min(xlo, __shfl_xor(xlo, o, kWave));
-      ylo = min(ylo, __shfl_xor(ylo, o, kWave));
-      xhi = max(xhi, __shfl_xor(xhi, o, kWave));
-      yhi = max(yhi, __shfl_xor(yhi, o, kWave));
-    }
-    if (gk == 0 && gl < L) {
-      const int H2 = LV_SEL(H2, gl), W2 = LV_SEL(W2, gl);
-      xlo = max(xlo - R, 0);
-      ylo = max(ylo - R, 0);
-      xhi = min(xhi + R + 1, W2 - 1);
-      yhi = min(yhi + R + 1, H2 - 1);
-      int bw = xhi - xlo + 1, bh = yhi - ylo + 1;
-      if (bw <= 0 || bh <= 0 || !idx_ok) bw = bh = 0;
-      geo[gl].xlo = xlo;
-      geo[gl].ylo = ylo;
-      geo[gl].bw = bw;
-      geo[gl].bh = bh;
-      geo[gl].ntile = (bw * bh + 15) >> 4;
-    }
-  }
-  wave_lds_sync();
-  // level order alternates between neighbouring workgroups (fine -> coarse /
-  // coarse -> fine), so co-resident edges are not all in the same phase
-  const bool rev = (blockIdx.x >> 3) & 1;
-  auto level_at = [&](int j) { return rev ? L - 1 - j : j; };
-  cum[0] = 0;
-#pragma unroll
-  for (int j = 0; j < kMaxL; j++) {
-    const int nt = (j < L) ? wave_uniform(geo[level_at(j)].ntile) : 0;
-    cum[j + 1] = cum[j] + ((nt <= kMaxTiles) ? nt : 0);
-  }
-  const int rx = lane >> 3, ry = lane & 7;
-  const int k0 = hw ? 5 : 0, kn = hw ? 4 : 5;  // this wave's patch pixels in the bilinear
-
-  // bilinear of level l for k in [k0, k0 + kn) (correlation_kernel.cu:260-271);
-  // fast: G holds the level's box tiles, else the raw [k][8][8] grid
-  auto bilinear = [&](int l, bool fast) __attribute__((always_inline)) {
-    const NhwcGeom* gg = geo + l;
-    const int xlo = wave_uniform(gg->xlo), ylo = wave_uniform(gg->ylo);
-    const int bw = wave_uniform(gg->bw), bh = wave_uniform(gg->bh);
-    const int cap = max(bw * bh - 1, 0);
-    float r[5], dxv[5], dyv[5];
-#pragma unroll
-    for (int u = 0; u < 5; u++) {
-      const int k = min(k0 + u, np - 1);
-      dxv[u] = gg->dx[k];
-      dyv[u] = gg->dy[k];
-      if (fast) {
-        const int gy = gg->y0[k] + ry - R - ylo, gx = gg->x0[k] + rx - R - xlo;
-        const bool in = gy >= 0 && gy < bh && gx >= 0 && gx < bw;
-        const float a = G[k * kBoxStride + min(max(gy * bw + gx, 0), cap)];
-        r[u] = in ? a : 0.f;
-      } else {
-        r[u] = G[k * 64 + ry * 8 + rx];
-      }
-    }
-    float v[5];
-#pragma unroll
-    for (int u = 0; u < 5; u++) {
-      const float r10 = __shfl_down(r[u], 1, kWave);
-      const float r01 = __shfl_down(r[u], 8, kWave);
-      const float r11 = __shfl_down(r[u], 9, kWave);
-      const float dx = dxv[u], dy = dyv[u];
-      float t = ((1.f - dx) * (1.f - dy)) * r[u];
-      t = t + (dx * (1.f - dy)) * r01;
-      t = t + ((1.f - dx) * dy) * r10;
-      t = t + (dx * dy) * r11;
-      v[u] = t;
-    }
-    if (rx < 7 && ry < 7) {
-#pragma unroll
-      for (int u = 0; u < 5; u++)
-        if (u < kn) obuf[((rx * 7 + ry) * 9 + k0 + u) * L + l] = v[u];
-    }
-  };
-  // zero this wave's rows of G over n entries per row
-  auto zero_rows = [&](int n, int stride) __attribute__((always_inline)) {
-    for (int u = 0; u < kn; u++)
-      for (int e = lane; e < n; e += kWave) G[(k0 + u) * stride + e] = 0.f;
-  };
-
-  const int nT = cum[kMaxL];
-  const float* pbase[kMaxL];
-  int prow[kMaxL], pbw[kMaxL], pnpx[kMaxL];
-  float prbw[kMaxL];
-#pragma unroll
-  for (int j = 0; j < kMaxL; j++) {
-    const int l = (j < L) ? level_at(j) : 0;
-    const NhwcGeom* gg = geo + l;
-    const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
-    const int bw0 = max(wave_uniform(gg->bw), 1);
-    pbw[j] = bw0;
-    pnpx[j] = bw0 * wave_uniform(gg->bh);
-    prbw[j] = 1.0f / (float)bw0;
-    prow[j] = W2 * C;
-    // an empty box reads the frame's first pixel (in range whatever the
-    // coordinates): the ring preload below is then unconditional
-    const bool empty = wave_uniform(gg->bw) <= 0 || wave_uniform(gg->bh) <= 0;
-    pbase[j] = static_cast<const float*>(LV_SEL(f2, l)) +
-               (((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 +
-                (empty ? 0 : (size_t)wave_uniform(gg->ylo) * W2 + wave_uniform(gg->xlo))) * C +
-               64 * hw;
-  }
-  auto pick = [](int j, auto a0, auto a1, auto a2, auto a3) __attribute__((always_inline)) {
-    return j == 0 ? a0 : j == 1 ? a1 : j == 2 ? a2 : a3;
-  };
-  auto load_tile = [&](u32x4 (&dst)[V], int i) __attribute__((always_inline)) {
-    i = min(i, max(nT - 1, 0));
-    const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
-    const int t = i - pick(j, 0, cum[1], cum[2], cum[3]);
-    const float* base = pick(j, pbase[0], pbase[1], pbase[2], pbase[3]);
-    const int row = pick(j, prow[0], prow[1], prow[2], prow[3]);
-    const int bw0 = pick(j, pbw[0], pbw[1], pbw[2], pbw[3]);
-    const int npx = pick(j, pnpx[0], pnpx[1], pnpx[2], pnpx[3]);
-    const float rbw = pick(j, prbw[0], prbw[1], prbw[2], prbw[3]);
-    const int px = min(16 * t + ai, max(npx - 1, 0));
-    const int rr = (int)(((float)px + 0.5f) * rbw), cc = px - rr * bw0;
-    const float* s = base + rr * row + cc * C + 4 * aq;
-#pragma unroll
-    for (int h = 0; h < V; h++) dst[h] = *reinterpret_cast<const u32x4*>(s + 16 * h);
-  };
-  // unconditional (a branch here makes the wait before the patch staging
-  // count only the patch loads on the no-tile path: it would drain the ring)
-  u32x4 ring[kSplitRing][V];
-#pragma unroll
-  for (int k = 0; k < kSplitRing; k++) {
-    load_tile(ring[k], k);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  build_A();
-  // G holds the other wave's staging until here
-  wg_lds_sync();
-  zero_rows(kBoxStride, kBoxStride);
-  wg_lds_sync();
-  // levels off the fast path first (raw grid straight into G, full channel sums)
-  for (int l = 0; l < L; l++) {
-    const int nt = wave_uniform(geo[l].ntile);
-    if (nt > kMaxTiles) {
-      const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
-      const float* f2 = static_cast<const float*>(LV_SEL(f2, l)) + ((size_t)b * N2 + jx) * H2 * W2 * C;
-      for (int e = threadIdx.x; e < np * D * D; e += kSplitThreads) {
-        const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
-        const int i1 = geo[l].y0[k] + yy - R, j1 = geo[l].x0[k] + xx - R;
-        float sacc = 0.f;
-        if (idx_ok && i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
-          const float* px = f2 + ((size_t)i1 * W2 + j1) * C;
-          const float* f1 = fmap1 + ((size_t)b * N1 + ix) * C * np;
-          for (int c = 0; c < C; c++) sacc += f1[(size_t)c * np + k] * px[c];
-        }
-        G[e] = sacc;
-      }
-      wg_lds_sync();
-      bilinear(l, false);
-      wg_lds_sync();
-      zero_rows(D * D, D * D);
-      wg_lds_sync();
-    } else if (nt == 0) {
-      bilinear(l, true);
-    }
-  }
-  if (nT > 0) {
-    auto step = [&](u32x4 (&cur)[V], int i) __attribute__((always_inline)) {
-      const bool live = i < nT;
-      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      if (live) {
-#pragma unroll
-        for (int h = 0; h < V; h += 2) {
-          const float4 c0 = __builtin_bit_cast(float4, cur[h]);
-          const float4 c1 = __builtin_bit_cast(float4, cur[h + 1]);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 0], c0.x, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 4], c1.x, acc1, 0, 0, 0);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 1], c0.y, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 5], c1.y, acc1, 0, 0, 0);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 2], c0.z, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 6], c1.z, acc1, 0, 0, 0);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 3], c0.w, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * h + 7], c1.w, acc1, 0, 0, 0);
-        }
-      }
-      load_tile(cur, i + kSplitRing);
-      if (!live) return;
-      const int j = (i >= cum[1]) + (i >= cum[2]) + (i >= cum[3]);
-      const int t = i - pick(j, 0, cum[1], cum[2], cum[3]), l = level_at(j);
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int row = 4 * aq + r;
-        if (row < np) atomicAdd(&G[row * kBoxStride + 16 * t + ai], acc0[r] + acc1[r]);
-      }
-      const int le = pick(j, cum[1], cum[2], cum[3], cum[4]);
-      if (i + 1 == le) {  // level complete in both waves: bilinear, then G zero again
-        wg_lds_sync();
-        bilinear(l, true);
-        wg_lds_sync();
-        zero_rows(16 * (le - pick(j, 0, cum[1], cum[2], cum[3])), kBoxStride);
-        wg_lds_sync();
-      }
-    };
-    for (int i = 0; i < nT; i += kSplitRing) {
-#pragma unroll
-      for (int k = 0; k < kSplitRing; k++) step(ring[k], i + k);
-    }
-  }
-  // ---- one contiguous [nout][L] row block per edge, both waves
-  wg_lds_sync();
-  float* dst = out + ((size_t)b * M + m) * nout * L;
-  if (((nout * L) & 3) == 0) {
-    for (int e = 4 * (int)threadIdx.x; e < nout * L; e += 4 * kSplitThreads)
-      *reinterpret_cast<float4*>(dst + e) = *reinterpret_cast<const float4*>(obuf + e);
-  } else {
-    for (int e = threadIdx.x; e < nout * L; e += kSplitThreads) dst[e] = obuf[e];
-  }
 }
 
 // [count, C, H, W] -> [count, H, W, C] (one 32 x 32 tile of (c, hw) per block)
@@ -932,14 +738,6 @@ __global__ void __launch_bounds__(256)
 
 using namespace dpvo;
 
-// DPVO_CORR_SPLIT=1 selects the channel-split kernel for fp32 (experiment, off:
-// 88.8 us against 57.5 us for the one-wave-per-edge kernel at cfg2,
-// profiles/r04_corr_split/)
-static bool corr_split_enabled() {
-  static const char* ov = getenv("DPVO_CORR_SPLIT");
-  return ov && ov[0] == '1';
-}
-
 DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
     const void* fmap1, const void* const* fmap2, const int* H2, const int* W2, const float* scale,
     int L, const float* coords, const int64_t* ii, const int64_t* jj, const int32_t* order, int B,
@@ -963,9 +761,7 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   // D * D <= 256 > kBoxStride only for R > 5, which the fast path covers)
   const int D = 2 * radius + 2;
   if (D * D > kBoxStride) return DPVO_ERR_UNSUPPORTED;
-  const size_t smem = sizeof(float) * kNhwcWaves * np * kBoxStride +
-                      sizeof(NhwcGeom) * kNhwcWaves * kMaxL +
-                      sizeof(float) * kNhwcWaves * corr_obuf_floats(np, radius, L);
+  const size_t smem = corr_nhwc_lds_bytes(np, radius, L);
   const long long units = (long long)B * M;
   unsigned grid = (unsigned)((units + kNhwcWaves - 1) / kNhwcWaves);
   const bool ordered = order && B == 1;
@@ -974,16 +770,6 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   const bool raw9 = np == 9 && radius == 3;  // DPVO: p = 3, R = 3
   const dim3 g(grid), blk(kNhwcWaves * kWave);
   hipStream_t st = as_stream(stream);
-  if (dtype == DPVO_F32 && raw9 && corr_split_enabled()) {
-    // one edge per 128-thread workgroup (channel-split waves)
-    unsigned g2 = (unsigned)units;
-    if (ordered) g2 = 8u * (unsigned)((g2 + 7) / 8);
-    const size_t smem2 = sizeof(float) * np * kBoxStride + sizeof(NhwcGeom) * 2 * kMaxL +
-                         sizeof(float) * corr_obuf_floats(np, radius, L);
-    hipLaunchKernelGGL(corr_split_kernel, dim3(g2), dim3(kSplitThreads), smem2, st,
-                       (const float*)fmap1, lv, L, coords, ii, jj, B, M, N1, N2, ord, out);
-    return launch_status();
-  }
   if (dtype == DPVO_F16) {
     const __half* f1 = (const __half*)fmap1;
     if (raw9)

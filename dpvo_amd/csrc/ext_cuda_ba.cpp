@@ -922,6 +922,10 @@ void kf_shift(torch::Tensor kf, int64_t M, torch::Tensor st, torch::Tensor ii, t
   int cap = 0;
   if (log) {
     TORCH_CHECK(poses && tstamps && delta_tstamps && delta_count, "delta log needs all buffers");
+    // the kernel ORs its delta-log overflow bit into counts[2] (keyframe.hip
+    // kf_delta_kernel): counts must hold the error word too
+    TORCH_CHECK(counts.numel() >= 3, "kf_shift with a delta log: counts needs >= 3 int32 words "
+                                     "(n, m, errors)");
     dl = delta_log->data_ptr<float>();
     dt = delta_tstamps->data_ptr<int64_t>();
     dc = const_cast<int32_t*>(dev_scalar(*delta_count, "delta_count"));
@@ -935,6 +939,56 @@ void kf_shift(torch::Tensor kf, int64_t M, torch::Tensor st, torch::Tensor ii, t
                              ptrs.data(), bytes.data(), ring.data(), (int)ptrs.size(), pp, ts, dl,
                              dt, dc, cap, current_stream()),
                "cuda_ba.kf_shift");
+}
+
+// CholeskySolver's device solve (dpvo/ba.py:13-38 -> torch.linalg.cholesky_ex +
+// cholesky_solve): batched over the leading dims, fp32 / fp64
+static void spd_shapes(const torch::Tensor& H, const torch::Tensor& B, int64_t& batch, int& n,
+                       int& k) {
+  check_device(H, "H");
+  check_device(B, "B");
+  TORCH_CHECK(H.dim() >= 2 && H.size(-1) == H.size(-2), "H must be [..., n, n]");
+  TORCH_CHECK(B.dim() == H.dim() && B.size(-2) == H.size(-1), "B must be [..., n, k]");
+  TORCH_CHECK(H.scalar_type() == B.scalar_type() &&
+                  (H.scalar_type() == torch::kFloat32 || H.scalar_type() == torch::kFloat64),
+              "H / B: float32 or float64, one dtype");
+  for (int64_t d = 0; d + 2 < H.dim(); d++)
+    TORCH_CHECK(H.size(d) == B.size(d), "H / B batch dims differ");
+  n = (int)H.size(-1);
+  k = (int)B.size(-1);
+  batch = n ? H.numel() / ((int64_t)n * n) : 0;
+}
+
+std::vector<torch::Tensor> spd_solve(torch::Tensor H, torch::Tensor B) {
+  int64_t batch;
+  int n, k;
+  spd_shapes(H, B, batch, n, k);
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(H.device());
+  H = H.contiguous();
+  B = B.contiguous();
+  auto L = torch::empty_like(H);
+  auto X = torch::empty_like(B);
+  std::vector<int64_t> bs(H.sizes().begin(), H.sizes().end() - 2);
+  auto info = torch::zeros(bs, H.options().dtype(torch::kInt32));
+  check_status(dpvo_spd_solve(H.data_ptr(), B.data_ptr(), L.data_ptr(), X.data_ptr(),
+                              info.data_ptr<int32_t>(), (int)batch, n, k, 1, dtype_code(H),
+                              current_stream()),
+               "cuda_ba.spd_solve");
+  return {X, L, info};
+}
+
+torch::Tensor spd_solve_factored(torch::Tensor L, torch::Tensor B) {
+  int64_t batch;
+  int n, k;
+  spd_shapes(L, B, batch, n, k);
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(L.device());
+  L = L.contiguous();
+  B = B.contiguous();
+  auto X = torch::empty_like(B);
+  check_status(dpvo_spd_solve(L.data_ptr(), B.data_ptr(), nullptr, X.data_ptr(), nullptr,
+                              (int)batch, n, k, 0, dtype_code(L), current_stream()),
+               "cuda_ba.spd_solve_factored");
+  return X;
 }
 
 // PatchGraph.edges_loop (patchgraph.py:65-91) gated as dpvo.py:984-988
@@ -1026,5 +1080,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "reproject + edge order by target frame (for cuda_corr.forward_levels(order=))");
   m.def("select_path", [](int mode) { check_status(dpvo_ba_select_path(mode), "select_path"); },
         "F-BA implementation: 0 auto, 2 multi-kernel, 4 large-graph, 5 window");
+  m.def("spd_solve", &spd_solve,
+        "batched SPD factor + solve (CholeskySolver, dpvo/ba.py:13-38): H [..., n, n] (lower "
+        "triangle read), B [..., n, k] -> [X, L (lower factor), info (first failed column, 0 = ok)]");
+  m.def("spd_solve_factored", &spd_solve_factored,
+        "X = (L L^T)^-1 B for a lower factor L from spd_solve (the backward's cholesky_solve)");
   m.attr("native_library") = dpvo_version();
 }

@@ -457,6 +457,22 @@ int dpvo_pg_remove_frame_dev(const int32_t* kf, int64_t* ii, int64_t* jj, int64_
                              float* target_b, int DIM, int* counts, int* pos, int max_edges,
                              void* stream);
 
+/* --------------------------------------------------------- SPD solve (training) */
+
+/* Batched dense SPD factor + solve: the device side of CholeskySolver
+   (dpvo/ba.py:13-38, which calls torch.linalg.cholesky_ex(H) and
+   cholesky_solve(b, U); block_solve 67-77 passes it the damped pose system).
+   batch items of H [n, n] (row-major; the lower triangle is read, as
+   cholesky_ex(upper=False)) and B [n, k]; dtype DPVO_F32 / DPVO_F64.
+   factor = 1: L = lower Cholesky factor (zeros above; required when
+   n x (n + k) elements exceed 160 KB of LDS: it is then the working copy),
+   X = H^-1 B, info[b] = first column whose pivot is not positive (1-based,
+   0 = success; LAPACK potrf / cholesky_ex semantics), X = 0 for a failed item.
+   factor = 0: H holds a lower factor from a factor = 1 call; X = (H H^T)^-1 B,
+   L and info must be null.  One 256-thread workgroup per item. */
+int dpvo_spd_solve(const void* H, const void* B, void* L, void* X, int32_t* info, int batch, int n,
+                   int k, int factor, int dtype, void* stream);
+
 /* ---------------------------------------------------------------- keyframe */
 
 /* DPVO.keyframe's decision (dpvo.py:586-599, 619-624) on the device.  st =

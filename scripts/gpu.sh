@@ -1,0 +1,77 @@
+#!/bin/bash
+# The one GPU driver (run through gpurun from the repo root):
+#     T=r05a scripts/gpu.sh tests smoke driver long prof
+# Each named step runs under its own time limit and writes
+# gpurun_out/${T}_<step>.txt (rocprof output under gpurun_out/${T}_<step>/).
+# The run stops at the first failing step: nothing more touches the GPU after
+# a fault, abort, segfault or time limit.
+#   tests      full GPU pytest suite           window  BA window / harness tests
+#   corrtests  corr + golden GPU tests         large   large-graph / global / sharded BA tests
+#   smoke      __graft_entry__.smoke()
+#   driver     bench.py exactly as the driver runs it (--steps 20 --warmup 5)
+#   long       bench.py --steps 300 --warmup 10 (no CPU baseline)
+#   bench      bench.py $BENCH_ARGS (full default run, CPU baseline included)
+#   prof       rocprofv3 --kernel-trace --stats over a 200-step bench (kernel table printed)
+#   profdrv    the same over the driver's 20-step command
+#   phases     BA window phase tables: cfg2 2 iterations, DPVO windows E=9850 / 3940 1 iteration
+#   probe      host enqueue time per call of a step, first after a sync vs steady
+#   stale      the stale-granule regression test; staledemo: its A/B on the round-4 tree
+#   corrmicro  A-CORR micro-bench (per-wave phase stamps) for each built variant
+#   cfg4       bench.py --sharded (cfg4 global BA, one rank)
+#   cfg4prof   rocprofv3 over the cfg4 bench
+#   pmcsq      BA/corr SQ + LDS counter passes (scripts/pmc.sh with PMC_GROUPS)
+#   traffic    corr FETCH_SIZE / WRITE_SIZE passes
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out
+T=${T:-run}
+mkdir -p $O
+PYT="python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu"
+run() {  # run <name> <limit-s> <cmd...>
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > $O/${T}_$name.txt 2>&1
+  local rc=$?
+  echo "step $name rc=$rc"
+  tail -4 $O/${T}_$name.txt
+  [ $rc -eq 0 ] || exit $rc
+}
+prof() {  # prof <name> <bench args...>
+  local name=$1; shift
+  run $name 400 rocprofv3 --kernel-trace --stats -d $O/${T}_$name -o run --output-format csv \
+    -- python bench.py --no-cpu-baseline "$@"
+  local f
+  f=$(find $O/${T}_$name -name "*kernel_stats.csv" | head -1)
+  python scripts/kstats.py "$f" 8 | tee $O/${T}_${name}_kstats.txt
+}
+for s in "$@"; do
+  case $s in
+    tests) run tests 900 $PYT tests ;;
+    window) run window 400 $PYT tests/test_ba_window_gpu.py tests/test_ba_gpu.py tests/test_update_harness_gpu.py ;;
+    corrtests) run corrtests 400 $PYT tests/test_corr_gpu.py tests/test_golden_gpu.py ;;
+    large) run large 500 $PYT tests/test_ba_large_gpu.py tests/test_global_ba_gpu.py tests/test_sharded_hip_gpu.py ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    driver) run driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    long) run long 300 python -u bench.py --steps 300 --warmup 10 --no-cpu-baseline ;;
+    bench) run bench 400 python -u bench.py ${BENCH_ARGS:-} ;;
+    prof) prof prof --steps 200 --warmup 10 ;;
+    profdrv) prof profdrv --steps 20 --warmup 5 ;;
+    phases)
+      run phases_cfg2 300 python -u scripts/ba_window_phases.py cfg2 2
+      run phases_dpvo25_1 300 python -u scripts/ba_window_phases.py 25 1
+      run phases_dpvo10_1 300 python -u scripts/ba_window_phases.py 10 1 ;;
+    probe) run probe 300 python -u scripts/host_enqueue_probe.py ;;
+    staledemo) run staledemo 400 python -u scripts/stale_granule_demo.py _r04tree . ;;
+    stale) run stale 400 $PYT tests/test_granule_stale_gpu.py ;;
+    corrmicro)  # scripts/micro/corr_bench variants (build them first on the CPU side)
+      for v in ${CORR_VARIANTS:-base exact nomma noload}; do
+        run corrmicro_$v 200 ./scripts/micro/corr_bench_$v 1 0 4 2048
+      done ;;
+    cfg4) run cfg4 300 python -u bench.py --sharded --steps 5 --warmup 2 ;;
+    cfg4prof) prof cfg4prof --sharded --steps 3 --warmup 1 ;;
+    pmcsq) run pmcsq 600 env PMC_GROUPS="${PMC_GROUPS:-SQ_WAIT_ANY SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES}" bash scripts/pmc.sh ;;
+    traffic) run traffic 400 env PMC_GROUPS="FETCH_SIZE WRITE_SIZE" bash scripts/pmc.sh ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+exit 0

@@ -15,22 +15,44 @@
 #include <vector>
 
 __device__ int64_t* g_stamps;  // [edges][16]
+// stamps go through a global-address-space pointer read once per wave at
+// kernel entry (CORR_TSTAMP_INIT): re-reading the __device__ variable per
+// stamp, or storing through a generic pointer, waits for every outstanding
+// tile load
+typedef __attribute__((address_space(1))) int64_t gi64;
 #define CORR_STAMP(slot)                                                     \
   do {                                                                       \
-    if (lane == 0) g_stamps[(size_t)edge * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
+    if (lane == 0) stp_[(size_t)edge * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
 #define CORR_STAMP_RT(slot)                                                  \
   do {                                                                       \
-    if (lane == 0) g_stamps[(size_t)edge * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    if (lane == 0) stp_[(size_t)edge * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
 #define CORR_STAMP_ID(slot)                                                  \
   do {                                                                       \
     if (lane == 0)                                                           \
-      g_stamps[(size_t)edge * 16 + (slot)] =                                 \
+      stp_[(size_t)edge * 16 + (slot)] =                                     \
           ((int64_t)__builtin_amdgcn_s_getreg(63508) << 32) |                 \
           (uint32_t)__builtin_amdgcn_s_getreg(63492);                         \
+  } while (0)
+
+// per-tile stamps of the first kTS edges: [edge][tile][3] (step start, loads
+// issued, G stored); s_memtime between sched barriers
+constexpr int kTS = 64, kTT = 32;
+__device__ int64_t* g_tst;
+// the buffer pointer is read once per wave (a per-stamp reload of the
+// __device__ variable would wait for every outstanding load)
+#define CORR_TSTAMP_INIT                                      \
+  gi64* const tst_ = (gi64*)(uintptr_t)g_tst;                 \
+  gi64* const stp_ = (gi64*)(uintptr_t)g_stamps
+#define CORR_TSTAMP(i, k)                                                            \
+  do {                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    if (lane == 0 && edge < kTS && (i) < kTT)                                        \
+      tst_[((size_t)edge * kTT + (i)) * 3 + (k)] = __builtin_amdgcn_s_memtime();     \
+    __builtin_amdgcn_sched_barrier(0);                                               \
   } while (0)
 
 #include "corr_nhwc.hip"
@@ -104,6 +126,10 @@ int main(int argc, char** argv) {
   const int parts = 1;
   hipMalloc(&dst, (size_t)E * 2 * 16 * 8);
   hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dst, sizeof(dst));
+  int64_t* dts;
+  hipMalloc(&dts, (size_t)kTS * kTT * 3 * 8);
+  hipMemset(dts, 0, (size_t)kTS * kTT * 3 * 8);
+  hipMemcpyToSymbol(HIP_SYMBOL(g_tst), &dts, sizeof(dts));
   // optional level subset: corr_bench <ordered> <first level> <count>
   const int l0 = argc > 2 ? atoi(argv[2]) : 0, Lr = argc > 3 ? atoi(argv[3]) : L;
   const void* f2[4] = {lvl[l0 % 4], lvl[(l0 + 1) % 4], lvl[(l0 + 2) % 4], lvl[(l0 + 3) % 4]};
@@ -216,5 +242,30 @@ int main(int argc, char** argv) {
   std::sort(life.begin(), life.end());
   printf("wave start offset median %lld p90 %lld max %lld; lifetime median %lld p90 %lld\n",
          st0[E / 2], st0[E * 9 / 10], st0[E - 1], life[E / 2], life[E * 9 / 10]);
+  {  // per-tile: a = start -> loads issued (wait + split + MFMA issue), b = -> G stored,
+     // c = G stored -> next step start (bilinear at level ends, loop)
+    std::vector<int64_t> t((size_t)kTS * kTT * 3);
+    hipMemcpy(t.data(), dts, t.size() * 8, hipMemcpyDeviceToHost);
+    std::vector<long long> A, Bv, Cv;
+    for (int e = 0; e < kTS; e++) {
+      printf("edge %d:", e < 4 ? e : -1);
+      for (int i = 0; i + 1 < kTT; i++) {
+        const int64_t* p = &t[((size_t)e * kTT + i) * 3];
+        const int64_t* q = p + 3;
+        if (!p[0] || !p[1] || !p[2]) break;
+        A.push_back(p[1] - p[0]);
+        Bv.push_back(p[2] - p[1]);
+        if (q[0]) Cv.push_back(q[0] - p[2]);
+        if (e < 4) printf(" [%lld %lld %lld]", (long long)(p[1] - p[0]), (long long)(p[2] - p[1]),
+                          q[0] ? (long long)(q[0] - p[2]) : -1LL);
+      }
+      if (e < 4) printf("\n");
+      else { printf("\r"); }
+    }
+    auto med = [](std::vector<long long> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0LL : v[v.size() / 2]; };
+    auto p90 = [](std::vector<long long> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0LL : v[v.size() * 9 / 10]; };
+    printf("\ntile: start->issued median %lld p90 %lld | ->G stored median %lld p90 %lld | ->next median %lld p90 %lld cyc\n",
+           med(A), p90(A), med(Bv), p90(Bv), med(Cv), p90(Cv));
+  }
   return 0;
 }

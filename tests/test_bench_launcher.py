@@ -5,6 +5,7 @@ consistency check."""
 import os
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -46,6 +47,17 @@ def test_launch_ranks_gloo_world2(tmp_path):
 def test_launch_ranks_reports_failure():
     code = "import os, sys; sys.exit(3 if os.environ['RANK'] == '1' else 0)"
     assert bench.launch_ranks(2, [], cmd=[sys.executable, "-c", code]) == 3
+
+
+def test_launch_ranks_failure_ends_waiting_ranks():
+    # rank 1 fails at once; rank 0 would wait (like a rank stuck in rendezvous):
+    # the launcher terminates it and reports rank 1's code without waiting it out
+    code = ("import os, sys, time\n"
+            "if os.environ['RANK'] == '1': sys.exit(5)\n"
+            "time.sleep(120)\n")
+    t = time.perf_counter()
+    assert bench.launch_ranks(2, [], cmd=[sys.executable, "-c", code]) == 5
+    assert time.perf_counter() - t < 60
 
 
 def test_gpus_world_size_mismatch_exits():
