@@ -129,9 +129,14 @@ int spd_launch(const void* H, const void* B, void* L, void* X, int32_t* info, in
   const size_t lds = sizeof(T) * ((size_t)n * n + (size_t)n * k);
   const int in_lds = lds <= kSpdLds - 64;
   if (!in_lds && factor && !L) return DPVO_ERR_INVALID;  // the HBM working copy is the factor buffer
-  if (in_lds)
-    (void)hipFuncSetAttribute((const void*)spd_kernel<T>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSpdLds);
+  if (in_lds && lds > 64 * 1024) {
+    // the dynamic LDS beyond the default 64 KB (the static fail flag sits on top)
+    if (hipFuncSetAttribute((const void*)spd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(kSpdLds - 64)) != hipSuccess) {
+      (void)hipGetLastError();  // not sticky: the launch reports its own status
+      return DPVO_ERR_LAUNCH;
+    }
+  }
   hipLaunchKernelGGL(spd_kernel<T>, dim3(batch), dim3(kSpdThreads), in_lds ? lds : 0,
                      as_stream(stream), (const T*)H, (const T*)B, (T*)L, (T*)X, (int*)info, n, k,
                      factor, in_lds);
