@@ -474,14 +474,26 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
         WSTAMP_DBG(57);
         const bool ok = chol6_m(m, L, ri);
         WSTAMP_DBG(58);
-        store_linv(s.Z + 36 * lblk(c1, c1), L, ri, lane);
-        WSTAMP_DBG(59);
         if (!ok && lane == 0) *fail = 1;
-        if (lane >= 6 && lane < nr) {
-          float lv[6];
-          fwd6(L, ri, v0, lv);
-          st_row(s.A + 36 * lblk(ia, c1) + 6 * xa, lv);
+        {
+          // ONE forward substitution per lane: lanes 0-5 solve for unit vectors
+          // (column `lane` of Linv = L^-1, stored with its zeros into Z), the
+          // other lanes for their panel row (L^-1 v0, stored into A); two
+          // back-to-back substitutions (store_linv, then the panel) were two
+          // dependent 21-FMA chains on the critical path of every block step
+          float rhs[6], z[6];
+#pragma unroll
+          for (int q = 0; q < 6; q++) rhs[q] = (lane < 6) ? ((q == lane) ? 1.0f : 0.0f) : v0[q];
+          fwd6(L, ri, rhs, z);
+          if (lane < 6) {
+            float* out = s.Z + 36 * lblk(c1, c1);
+#pragma unroll
+            for (int x = 0; x < 6; x++) out[6 * x + lane] = z[x];
+          } else if (lane < nr) {
+            st_row(s.A + 36 * lblk(ia, c1) + 6 * xa, z);
+          }
         }
+        WSTAMP_DBG(59);
         if (lane + 64 < nr) {
           float lv[6];
           fwd6(L, ri, v1, lv);

@@ -17,6 +17,7 @@
 #   probe      host enqueue time per call of a step, first after a sync vs steady
 #   stale      the stale-granule regression test; staledemo: its A/B on the round-4 tree
 #   corrmicro  A-CORR micro-bench (per-wave phase stamps) for each built variant
+#   launchprof rocprof kernel durations of the fused start-of-update launch and its parts
 #   cfg4       bench.py --sharded (cfg4 global BA, one rank)
 #   cfg4prof   rocprofv3 over the cfg4 bench
 #   pmcsq      BA/corr SQ + LDS counter passes (scripts/pmc.sh with PMC_GROUPS)
@@ -67,6 +68,11 @@ for s in "$@"; do
       for v in ${CORR_VARIANTS:-base exact nomma noload}; do
         run corrmicro_$v 200 ./scripts/micro/corr_bench_$v 1 0 4 2048
       done ;;
+    launchprof)  # kernel durations of the update's first launch and its parts
+      run launchprof 300 rocprofv3 --kernel-trace --stats -d $O/${T}_launchprof -o run --output-format csv \
+        -- python scripts/reproject_launch_bench.py cfg2 dpvo25
+      python scripts/kstats.py "$(find $O/${T}_launchprof -name '*kernel_stats.csv' | head -1)" 12 \
+        | tee $O/${T}_launchprof_kstats.txt ;;
     cfg4) run cfg4 300 python -u bench.py --sharded --steps 5 --warmup 2 ;;
     cfg4prof) prof cfg4prof --sharded --steps 3 --warmup 1 ;;
     pmcsq) run pmcsq 600 env PMC_GROUPS="${PMC_GROUPS:-SQ_WAIT_ANY SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES}" bash scripts/pmc.sh ;;
