@@ -30,7 +30,7 @@ INCLUDE = os.path.join(REPO, "include")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("DPVO_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["corr.hip", "corr_nhwc.hip", "ba.hip", "ba_window.hip", "ba_large.hip", "lie.hip", "pgo.hip", "pg.hip",
+HIP_SOURCES = ["corr.hip", "corr_nhwc.hip", "corr_nchw.hip", "ba.hip", "ba_window.hip", "ba_large.hip", "lie.hip", "pgo.hip", "pg.hip",
                "keyframe.hip", "spd_solve.hip"]
 EXTENSIONS = {
     "cuda_corr": "ext_cuda_corr.cpp",

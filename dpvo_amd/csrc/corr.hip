@@ -19,6 +19,13 @@
 
 namespace dpvo {
 
+// corr_nchw.hip: the matrix-core forward for NCHW fp16 levels (returns
+// DPVO_ERR_UNSUPPORTED outside its shape; the VALU kernels below take those)
+int corr_nchw_mma(const void* fmap1, const void* const* fmap2, const int* H2, const int* W2,
+                  const float* scale, int L, bool use_scale, const float* coords,
+                  const int64_t* ii, const int64_t* jj, int B, int M, int C, int np, int N1,
+                  int N2, int R, int dtype, void* out_t, float* out_f, hipStream_t s);
+
 constexpr int kCorrWaves = 4;       // waves (edges) per workgroup
 constexpr int kBoxPx = 2 * kWave;   // bounding-box pixels per wave (2 per lane)
 
@@ -522,6 +529,11 @@ DPVO_EXPORT int dpvo_corr_forward(const void* fmap1, const void* fmap2, const fl
   if (!fmap1 || !fmap2 || !coords || !ii || !jj || !out) return DPVO_ERR_INVALID;
   hipStream_t s = as_stream(stream);
   const int np = H * W;
+  if (dtype == DPVO_F16) {
+    const int st = corr_nchw_mma(fmap1, &fmap2, &H2, &W2, nullptr, 1, false, coords, ii, jj, B,
+                                 M, C, np, N1, N2, radius, dtype, out, nullptr, s);
+    if (st != DPVO_ERR_UNSUPPORTED) return st;
+  }
   switch (dtype) {
     case DPVO_F32:
       return launch_corr_fwd<float>(fmap1, fmap2, coords, ii, jj, B, M, C, np, N1, N2, H2, W2,
@@ -553,6 +565,11 @@ DPVO_EXPORT int dpvo_corr_forward_levels(const void* fmap1, const void* const* f
   }
   hipStream_t s = as_stream(stream);
   const int np = H * W;
+  if (dtype == DPVO_F16) {
+    const int st = corr_nchw_mma(fmap1, fmap2, H2, W2, scale, L, true, coords, ii, jj, B, M, C,
+                                 np, N1, N2, radius, dtype, nullptr, out, s);
+    if (st != DPVO_ERR_UNSUPPORTED) return st;
+  }
   switch (dtype) {
     case DPVO_F32:
       return launch_corr_fwd_levels<float>(fmap1, lv, L, coords, ii, jj, B, M, C, np, N1, N2,

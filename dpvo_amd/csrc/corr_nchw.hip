@@ -1,0 +1,371 @@
+// corr_nchw.hip -- A-CORR on the matrix cores for NCHW fp16 feature maps: the
+// layout DPVO allocates (dpvo.py:111-112, fp16 under its default
+// MIXED_PRECISION runtime), behind the unchanged per-level entry
+// (correlation.cpp:32-38 -> cuda_corr.forward, called per level at
+// dpvo.py:462-465) and the fused multi-level one.
+//
+// Same semantics as corr.hip (correlation_kernel.cu:82-175 + 232-272) and the
+// same per-edge GEMM as corr_nhwc.hip,
+//     G[k][px] = sum_c f1[c][k] * f2[c][px]     over the union box of the
+// edge's p*p windows, but a channel-plane box row is only ~10 contiguous
+// halves, so a B fragment (8 channels of one pixel per lane) cannot come
+// straight from HBM.  Each wave (one edge, one level):
+//   * loads the box 32 channels at a time: per channel, bh rows x npr aligned
+//     pieces of G halves (16-B pieces when W2 % 8 == 0, 8-B when W2 % 4 == 0);
+//     lane = (channel cl = lane & 31, row parity hf = lane >> 5), so the
+//     per-piece address is one lane base plus a wave-uniform offset;
+//   * writes them to an LDS image [32 channels][P pixels], P = bh x Wp
+//     (Wp = npr x G) padded to an ODD number of 16-pixel tiles;
+//   * reads B fragments with ds_read_b64_tr_b16 (gfx950's transposing LDS
+//     read: a 16-lane group receives 4 channel rows x 16 pixels one pixel per
+//     lane, i.e. the channel-major image arrives in the MFMA's k-per-lane
+//     layout).  The 8 channel rows one 32-lane half reads are P/2 = 8 x odd
+//     dwords apart, so they fall on 8 disjoint 8-bank groups: conflict-free;
+//   * multiplies with v_mfma_f32_16x16x32_f16 (fp32 accumulation, the
+//     documented deviation of every fp16 path here), one accumulator tile per
+//     16 image pixels (pad pixels produce columns nobody reads);
+//   * while the next 32-channel chunk's loads are in flight;
+//   * then the bilinear + permute from G in LDS, as corr.hip.
+// K order of one 32-channel chunk u: lane group g (= lane >> 4) holds, in
+// element j of its fragment, channel 32u + 4g + j (j < 4) or 32u + 16 + 4g +
+// j - 4 (j >= 4) -- the rows of its two transposed reads -- in both the A
+// (gmap patch) and the B (box) fragment.
+#include "common.hpp"
+
+namespace dpvo {
+namespace {
+
+constexpr int kNcWaves = 4;      // edges per workgroup
+constexpr int kNcC = 128;        // channels (DPVO fmap width)
+constexpr int kNcChunk = 32;     // channels per LDS image (one MFMA K step)
+constexpr int kNcChunks = kNcC / kNcChunk;
+constexpr int kNcMaxTiles = 17;  // odd; box image <= 272 px
+constexpr int kNcMaxPx = 16 * kNcMaxTiles;
+constexpr int kNcNpMax = 16;     // p * p <= 16 (one MFMA row tile)
+constexpr int kNcMaxL = 4;
+// per wave: the image (reused as G: np x P floats <= 16 x 272, or the slow
+// path's np x D x D <= 16 x 256) + the patch geometry
+constexpr int kNcImgBytes = kNcChunk * kNcMaxPx * 2;
+
+struct NcLevels {
+  const __half* f2[kNcMaxL];  // [B, N2, C, H2, W2]
+  int H2[kNcMaxL], W2[kNcMaxL], g[kNcMaxL];
+  float scale[kNcMaxL];
+};
+
+struct NcGeom {
+  int x0[kNcNpMax], y0[kNcNpMax];
+  float dx[kNcNpMax], dy[kNcNpMax];
+};
+constexpr int kNcWaveBytes = kNcImgBytes + (int)sizeof(NcGeom);
+static_assert(kNcWaveBytes % 16 == 0, "per-wave LDS carve must keep 16-B alignment");
+
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+template <int G>
+struct NcPiece;
+template <>
+struct NcPiece<8> { typedef u4 type; };  // 16 B
+template <>
+struct NcPiece<4> { typedef u2 type; };  // 8 B
+
+// global-address-space load (a generic pointer would be a flat load, counted
+// in both vmcnt and lgkmcnt)
+template <typename V>
+__device__ __forceinline__ V ldg(const void* p) {
+  return *reinterpret_cast<const __attribute__((address_space(1))) V*>(reinterpret_cast<uintptr_t>(p));
+}
+
+__device__ __forceinline__ h4 tr_read(const char* lds) {
+  const s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s4*)(lds));
+  return __builtin_bit_cast(h4, v);
+}
+
+template <typename X>
+__device__ __forceinline__ X nc_sel(int l, X a, X b, X c, X d) {
+  return l == 0 ? a : l == 1 ? b : l == 2 ? c : d;
+}
+
+// One edge at one level.  G = piece width in halves (8 or 4).
+template <int G>
+__device__ __forceinline__ void nc_edge(const __half* __restrict__ fmap1,
+                                        const __half* __restrict__ f2lvl, int H2, int W2,
+                                        float scale, bool use_scale,
+                                        const float* __restrict__ coords, int b, int m, int ix,
+                                        int jx, int M, int np, int N1, int N2, int R, char* wlds,
+                                        __half* __restrict__ out_t, float* __restrict__ out_f,
+                                        int out_stride, int out_off) {
+  // pieces per lane per chunk: row pairs x pieces per row (18 x 16 B or 35 x 8 B)
+  constexpr int kNpr = G == 8 ? 3 : 5, kRows2 = G == 8 ? 6 : 7;
+  using PT = typename NcPiece<G>::type;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int D = 2 * R + 2, Dp = D - 1;
+  float* Gs = reinterpret_cast<float*>(wlds);
+  NcGeom* geo = reinterpret_cast<NcGeom*>(wlds + kNcImgBytes);
+
+  // ---- geometry: lane k < np takes patch pixel k (floor / frac) ----
+  float cv = 0.f;
+  if (lane < 2 * np) {
+    cv = coords[((size_t)b * M + m) * 2 * np + lane];
+    if (use_scale) cv = cv / scale;  // coords / scale (dpvo.py:462-463)
+  }
+  const float cy = __shfl(cv, min(lane + np, kWave - 1), kWave);
+  int xf = 0x7fffffff, yf = 0x7fffffff, xg = -0x7fffffff, yg = -0x7fffffff;
+  if (lane < np) {
+    xf = xg = ifloor_safe(cv);
+    yf = yg = ifloor_safe(cy);
+    geo->x0[lane] = xf;
+    geo->y0[lane] = yf;
+    geo->dx[lane] = cv - floorf(cv);  // correlation_kernel.cu:262
+    geo->dy[lane] = cy - floorf(cy);
+  }
+  // union bounding box of all windows, clipped to the map (wave-uniform)
+  const int xlo = wave_uniform(max(wave_min_i(xf) - R, 0));
+  const int ylo = wave_uniform(max(wave_min_i(yf) - R, 0));
+  const int xhi = wave_uniform(min(wave_max_i(xg) + R + 1, W2 - 1));
+  const int yhi = wave_uniform(min(wave_max_i(yg) + R + 1, H2 - 1));
+  wave_lds_sync();
+  const bool idx_ok = ix >= 0 && ix < N1 && jx >= 0 && jx < N2;
+  int bw = xhi - xlo + 1, bh = yhi - ylo + 1;
+  if (bw <= 0 || bh <= 0 || !idx_ok) bw = bh = 0;
+  const int npx = bw * bh;
+  // image geometry: rows start at the G-aligned column xs <= xlo
+  const int xs = xlo & ~(G - 1);
+  const int npr = npx > 0 ? (xhi - xs) / G + 1 : 0;  // pieces per box row
+  const int Wp = npr * G;
+  const int nt = ((bh * Wp + 15) >> 4) | 1;  // odd tile count (bank-conflict-free reads)
+  const int rows2 = (bh + 1) >> 1;          // row pairs
+  const bool fast = npx > 0 && nt <= kNcMaxTiles && rows2 <= kRows2 && npr <= kNpr;
+  const int P = nt * 16;
+  const int xoff = xlo - xs;
+  const size_t HW2 = (size_t)H2 * W2;
+
+  if (fast) {
+    const __half* f2 = f2lvl + ((size_t)b * N2 + jx) * kNcC * HW2;
+    const __half* f1 = fmap1 + ((size_t)b * N1 + ix) * kNcC * np;
+    const int cl = lane & 31, hf = lane >> 5;
+    const __half* src0 = f2 + (size_t)cl * HW2 + (size_t)ylo * W2 + xs;
+    PT buf[kRows2 * kNpr];
+    // chunk u's pieces: lane (cl, hf) loads channel 32u + cl, box rows
+    // hf + 2 r2 (an odd box height's last hf = 1 row re-reads the row above:
+    // loaded, not written), pieces pc of G halves.  Row and piece loops are
+    // compile-time (per-piece offsets: one scalar per row pair + immediates)
+    auto issue = [&](int u) __attribute__((always_inline)) {
+      const __half* s = src0 + (size_t)u * kNcChunk * HW2;
+#pragma unroll
+      for (int r2 = 0; r2 < kRows2; r2++) {
+        if (r2 < rows2) {
+          const __half* sr = s + (size_t)(2 * r2 + (hf && 2 * r2 + 1 < bh ? 1 : 0)) * W2;
+#pragma unroll
+          for (int pc = 0; pc < kNpr; pc++)
+            if (pc < npr) buf[r2 * kNpr + pc] = ldg<PT>(sr + pc * G);
+        }
+      }
+    };
+    char* wb = wlds + (cl * P + hf * Wp) * 2;  // the lane's first piece in the image
+    auto stage = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int r2 = 0; r2 < kRows2; r2++) {
+        if (r2 < rows2 && hf + 2 * r2 < bh) {
+#pragma unroll
+          for (int pc = 0; pc < kNpr; pc++)
+            if (pc < npr)
+              *reinterpret_cast<PT*>(wb + (2 * r2 * Wp + pc * G) * 2) = buf[r2 * kNpr + pc];
+        }
+      }
+    };
+
+    // gmap patch [C][np] (16-B units, C * np * 2 is a multiple of 16) -> LDS
+    // -> A fragments; its loads overlap chunk 0's
+    constexpr int kRA = (kNcC * kNcNpMax / 8 + kWave - 1) / kWave;
+    const int n16 = kNcC * np / 8;
+    u4 pa[kRA];
+#pragma unroll
+    for (int r = 0; r < kRA; r++) pa[r] = ldg<u4>(f1 + 8 * min(lane + kWave * r, n16 - 1));
+    issue(0);
+#pragma unroll
+    for (int r = 0; r < kRA; r++)
+      if (lane + kWave * r < n16) reinterpret_cast<u4*>(wlds)[lane + kWave * r] = pa[r];
+    wave_lds_sync();
+    const int g4 = lane >> 4, am = lane & 15;
+    h8 A[kNcChunks];
+    {
+      const _Float16* ph = reinterpret_cast<const _Float16*>(wlds);
+      const bool arow = am < np;
+#pragma unroll
+      for (int u = 0; u < kNcChunks; u++)
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const int c = kNcChunk * u + (j < 4 ? 4 * g4 + j : 16 + 4 * g4 + j - 4);
+          A[u][j] = arow ? ph[c * np + am] : (_Float16)0.0f;
+        }
+    }
+    wave_lds_sync();  // patch read: the image may overwrite it
+
+    // transposed-read address of lane (g4, row q' = (lane >> 2) & 3, col 4 (lane & 3))
+    const char* ta = wlds + ((4 * g4 + ((lane >> 2) & 3)) * P + 4 * (lane & 3)) * 2;
+    const int ta1 = 16 * P * 2;  // the second read: channel rows 16 + 4 g4 + q'
+    f4 acc[kNcMaxTiles];
+#pragma unroll
+    for (int t = 0; t < kNcMaxTiles; t++) acc[t] = (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < kNcChunks; u++) {
+      stage();
+      wave_lds_sync();
+      if (u + 1 < kNcChunks) issue(u + 1);
+#pragma unroll
+      for (int t = 0; t < kNcMaxTiles; t++) {
+        if (t < nt) {
+          const h4 b0 = tr_read(ta + 32 * t), b1 = tr_read(ta + ta1 + 32 * t);
+          const h8 bb = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[u], bb, acc[t], 0, 0, 0);
+        }
+      }
+      wave_lds_sync();  // this chunk's reads before the next chunk's writes
+    }
+    // D tile t: lane (col n = lane & 15, rows 4 g4 + r) -> G[k][16 t + n]
+#pragma unroll
+    for (int t = 0; t < kNcMaxTiles; t++) {
+      if (t < nt) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int k = 4 * g4 + r;
+          if (k < np) Gs[k * P + 16 * t + am] = acc[t][r];
+        }
+      }
+    }
+  } else if (npx > 0) {
+    // ---- rare: windows too spread for the image; raw[k][yy][xx] directly ----
+    const __half* f2 = f2lvl + ((size_t)b * N2 + jx) * kNcC * HW2;
+    const __half* f1 = fmap1 + ((size_t)b * N1 + ix) * kNcC * np;
+    const int nraw = np * D * D;
+    for (int e = lane; e < nraw; e += kWave) {
+      const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
+      const int i1 = geo->y0[k] + yy - R, j1 = geo->x0[k] + xx - R;
+      float s = 0.f;
+      if (i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
+        const __half* p2 = f2 + (size_t)i1 * W2 + j1;
+        for (int c = 0; c < kNcC; c++)
+          s += __half2float(f1[c * np + k]) * __half2float(p2[(size_t)c * HW2]);
+      }
+      Gs[e] = s;
+    }
+  }
+  wave_lds_sync();
+
+  // ---- bilinear + permute, fused into the store (correlation_kernel.cu:260-271) ----
+  const int total = Dp * Dp * np;
+  const size_t ebase = ((size_t)b * M + m) * total;
+  for (int o = lane; o < total; o += kWave) {
+    const int k = o % np, t = o / np, yy = t % Dp, xx = t / Dp;
+    float r00, r01, r10, r11;
+    if (fast || npx == 0) {
+      const int gy = geo->y0[k] + yy - R - ylo, gx = geo->x0[k] + xx - R - xlo;
+      const float* g = Gs + k * P + xoff;
+      auto at = [&](int y, int x) -> float {
+        return (y >= 0 && y < bh && x >= 0 && x < bw) ? g[y * Wp + x] : 0.f;
+      };
+      r00 = at(gy, gx);
+      r01 = at(gy, gx + 1);
+      r10 = at(gy + 1, gx);
+      r11 = at(gy + 1, gx + 1);
+    } else {
+      const float* g = Gs + k * D * D;
+      r00 = g[yy * D + xx];
+      r01 = g[yy * D + xx + 1];
+      r10 = g[(yy + 1) * D + xx];
+      r11 = g[(yy + 1) * D + xx + 1];
+    }
+    const float dx = geo->dx[k], dy = geo->dy[k];
+    float v = ((1.f - dx) * (1.f - dy)) * r00;
+    v = v + (dx * (1.f - dy)) * r01;
+    v = v + ((1.f - dx) * dy) * r10;
+    v = v + (dx * dy) * r11;
+    if (out_t)
+      out_t[ebase + o] = __float2half(v);
+    else
+      out_f[(ebase + o) * out_stride + out_off] = v;
+  }
+  wave_lds_sync();
+}
+
+__global__ void __launch_bounds__(kNcWaves* kWave, 2)  // 2 workgroups (8 waves) per CU
+    corr_nchw_kernel(const __half* __restrict__ fmap1, NcLevels lv, int use_scale,
+                     const float* __restrict__ coords, const int64_t* __restrict__ ii,
+                     const int64_t* __restrict__ jj, int B, int M, int np, int N1, int N2, int R,
+                     int L, __half* __restrict__ out_t, float* __restrict__ out_f) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wid = wave_uniform(threadIdx.x / kWave);
+  char* wlds = smem + wid * kNcWaveBytes;
+  const int unit = blockIdx.x * kNcWaves + wid;
+  if (unit >= B * M) return;  // waves are independent: no block barrier below
+  const int l = blockIdx.y;
+  const int b = unit / M, m = unit % M;
+  const int ix = wave_uniform((int)ii[m]), jx = wave_uniform((int)jj[m]);
+  const __half* f2 = nc_sel(l, lv.f2[0], lv.f2[1], lv.f2[2], lv.f2[3]);
+  const int H2 = nc_sel(l, lv.H2[0], lv.H2[1], lv.H2[2], lv.H2[3]);
+  const int W2 = nc_sel(l, lv.W2[0], lv.W2[1], lv.W2[2], lv.W2[3]);
+  const int g = nc_sel(l, lv.g[0], lv.g[1], lv.g[2], lv.g[3]);
+  const float s = nc_sel(l, lv.scale[0], lv.scale[1], lv.scale[2], lv.scale[3]);
+  if (g == 8)
+    nc_edge<8>(fmap1, f2, H2, W2, s, use_scale != 0, coords, b, m, ix, jx, M, np, N1, N2, R, wlds,
+               out_t, out_f, L, l);
+  else
+    nc_edge<4>(fmap1, f2, H2, W2, s, use_scale != 0, coords, b, m, ix, jx, M, np, N1, N2, R, wlds,
+               out_t, out_f, L, l);
+}
+
+}  // namespace
+
+// The matrix-core NCHW fp16 forward, or DPVO_ERR_UNSUPPORTED when the call is
+// outside its shape (then the caller runs corr.hip's VALU kernel): fp16, C =
+// 128, p*p <= 16, L <= 4, every level W2 % 4 == 0 with a piece-aligned base.
+// out_t: [B, M, Dp, Dp, p, p] fp16 (L = 1); else out_f [.., L] float32.
+int corr_nchw_mma(const void* fmap1, const void* const* fmap2, const int* H2, const int* W2,
+                  const float* scale, int L, bool use_scale, const float* coords,
+                  const int64_t* ii, const int64_t* jj, int B, int M, int C, int np, int N1,
+                  int N2, int R, int dtype, void* out_t, float* out_f, hipStream_t s) {
+  if (dtype != DPVO_F16 || C != kNcC || np < 1 || np > kNcNpMax || L < 1 || L > kNcMaxL ||
+      R < 0 || R > 7)
+    return DPVO_ERR_UNSUPPORTED;
+  if (out_t && L != 1) return DPVO_ERR_INVALID;
+  if (reinterpret_cast<uintptr_t>(fmap1) % 16) return DPVO_ERR_UNSUPPORTED;
+  NcLevels lv = {};
+  for (int l = 0; l < L; l++) {
+    const uintptr_t p = reinterpret_cast<uintptr_t>(fmap2[l]);
+    int g = 0;
+    if (W2[l] % 8 == 0 && p % 16 == 0) g = 8;
+    else if (W2[l] % 4 == 0 && p % 8 == 0) g = 4;
+    if (!g || H2[l] <= 0) return DPVO_ERR_UNSUPPORTED;
+    lv.f2[l] = reinterpret_cast<const __half*>(fmap2[l]);
+    lv.H2[l] = H2[l];
+    lv.W2[l] = W2[l];
+    lv.g[l] = g;
+    lv.scale[l] = scale ? scale[l] : 1.0f;
+  }
+  if ((long long)B * M == 0) return DPVO_OK;
+  static bool attr = false;  // 4 x 17.7 KB per workgroup: above the default 64 KB
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)corr_nchw_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kNcWaves * kNcWaveBytes) != hipSuccess) {
+      (void)hipGetLastError();  // not sticky: report it here, not at a later launch
+      return DPVO_ERR_LAUNCH;
+    }
+    attr = true;
+  }
+  const dim3 grid((unsigned)(((long long)B * M + kNcWaves - 1) / kNcWaves), L),
+      block(kNcWaves * kWave);
+  hipLaunchKernelGGL(corr_nchw_kernel, grid, block, (size_t)kNcWaves * kNcWaveBytes, s,
+                     (const __half*)fmap1, lv, use_scale ? 1 : 0, coords, ii, jj, B, M, np, N1,
+                     N2, R, L, (__half*)out_t, out_f);
+  return launch_status();
+}
+
+}  // namespace dpvo

@@ -378,3 +378,110 @@ def test_insert_frame_fp16(gpu, H, W, scales):
         ref = fmap if s == 1 else torch.nn.functional.avg_pool2d(fmap[None].float(), s, s)[0].half()
         assert torch.equal(p[0, 1], ref), s
         assert bool((p[0, [0, 2]] == 7.0).all())
+
+
+# ---- NCHW fp16 levels: matrix-core path (corr_nchw.hip) ----
+# DPVO's own pyramid (dpvo.py:111-112: contiguous NCHW, fp16 under the default
+# MIXED_PRECISION) through the unchanged per-level entry.  fp16 x fp16
+# products are exact in fp32 and accumulate in fp32; the output is rounded
+# once to fp16, so against the fp64 oracle on the same fp16 inputs each value
+# is within one fp16 rounding (2^-11 relative, 2^-10 allowed) plus fp32
+# summation noise (2e-5 of max|ref|).
+def _close_f16(out, ref):
+    out = np.asarray(out, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert out.shape == ref.shape
+    tol = 2.0 ** -10 * np.abs(ref) + 2e-5 * max(1.0, np.abs(ref).max() if ref.size else 1.0)
+    bad = np.abs(out - ref) > tol
+    assert not bad.any(), (np.abs(out - ref).max(), int(bad.sum()))
+
+
+def _f16_inputs(f1, f2):
+    return f1.astype(np.float16), f2.astype(np.float16)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(),                                   # W2 = 32: 16-B pieces
+    dict(W2=36),                              # W2 % 8 == 4: 8-B pieces
+    dict(W2=30, M=40),                        # W2 % 4 != 0: VALU kernel
+    dict(R=0), dict(R=1), dict(R=2),
+    dict(R=7),                                # box too wide for the image: raw path
+    dict(p=1), dict(p=2), dict(p=4),
+    dict(Hp=2, Wp=3),
+    dict(spread=1.0, M=120),                  # image and raw edges mixed
+    dict(spread=4.0),
+    dict(far=0.5),                            # windows outside the map
+    dict(B=2, M=11),
+    dict(C=64, M=9),                          # C != 128: VALU kernel
+    dict(H2=5, W2=8, M=21),                   # tiny map: every window clipped
+    dict(M=300, H2=40, W2=48),
+])
+def test_nchw_fp16_forward_matches_oracle(cc, gpu, kw):
+    f1, f2, co, ii, jj, R = _case(21, **kw)
+    h1, h2 = _f16_inputs(f1, f2)
+    out, = cc.forward(_t(h1, gpu), _t(h2, gpu), _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R)
+    assert out.dtype == torch.float16
+    ref = oracle.corr_fwd(h1.astype(np.float64), h2.astype(np.float64), co, ii, jj, R)
+    _close_f16(out.cpu().numpy(), ref)
+
+
+def test_nchw_fp16_unaligned_level_base(cc, gpu):
+    """A level whose base is only 8-B aligned (a view at an odd offset) takes
+    8-B pieces; a 2-B aligned one the VALU kernel: same results."""
+    f1, f2, co, ii, jj, R = _case(22, M=90, H2=24, W2=32)
+    h1, h2 = _f16_inputs(f1, f2)
+    ref = oracle.corr_fwd(h1.astype(np.float64), h2.astype(np.float64), co, ii, jj, R)
+    for shift in (4, 1):
+        buf = torch.zeros(h2.size + shift, dtype=torch.float16, device=gpu)
+        lv = buf[shift:].view(h2.shape)
+        lv.copy_(_t(h2, gpu))
+        out, = cc.forward(_t(h1, gpu), lv, _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R)
+        _close_f16(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("levels", [(1, 4), (1, 2, 4, 8)])
+def test_nchw_fp16_levels_match_oracle(gpu, levels):
+    """corr_levels on an NCHW fp16 pyramid (float32 output): every level on
+    the matrix-core kernel (W2 = 64, 32, 16, 8)."""
+    from dpvo_amd import altcorr
+
+    f1, f2, co, ii, jj, R = _case(23, M=150, C=128, H2=48, W2=64)
+    h1, h2 = _f16_inputs(f1, f2)
+    lv1 = _t(h2, gpu)
+    pyr = [lv1 if s == 1 else
+           torch.nn.functional.avg_pool2d(lv1[0].float(), s, s).half().unsqueeze(0).contiguous()
+           for s in levels]
+    out = altcorr.corr_levels(_t(h1, gpu), pyr, _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R,
+                              scales=levels)
+    out = out.view(1, len(ii), 2 * R + 1, 2 * R + 1, 3, 3, len(levels)).cpu().numpy()
+    for l, s in enumerate(levels):
+        ref = oracle.corr_fwd(h1.astype(np.float64), pyr[l].double().cpu().numpy(), co / s, ii,
+                              jj, R)
+        _close(out[..., l], ref, 2e-5)
+
+
+def test_nchw_fp16_cfg2_matches_channels_last(cc, gpu):
+    """The drop-in call at full cfg2 size (2048 edges, 36-frame fp16 ring,
+    dpvo.py:462-465 verbatim) agrees with the channels-last kernel on the same
+    data to one fp16 ulp, and with the oracle on a sample of edges."""
+    from dpvo_amd import fastba, synthetic
+
+    G = synthetic.make_config("cfg2", seed=7)
+    D = G.to(gpu)
+    mem, levels = 36, (1, 4)
+    coords = fastba.reproject(D.poses, D.patches, D.intrinsics, D.ii, D.jj, D.kk)
+    pyr = [p.half() for p in synthetic.make_features(mem=mem, C=128, levels=levels, seed=3,
+                                                      device=gpu)]
+    gmap = (0.25 * torch.randn(1, mem * G.M, 128, 3, 3, device=gpu)).half()
+    kk1, jj1 = D.kk % (mem * G.M), D.jj % mem
+    sel = np.arange(0, G.E, 37)
+    for l, s in enumerate(levels):
+        a, = cc.forward(gmap, pyr[l], coords / s, kk1, jj1, 3)
+        b, = cc.forward(gmap, synthetic.channels_last(pyr[l]), coords / s, kk1, jj1, 3)
+        a64, b64 = a.double().cpu().numpy(), b.double().cpu().numpy()
+        tol = 2.0 ** -10 * np.abs(b64) + 1e-6 * np.abs(b64).max()
+        assert (np.abs(a64 - b64) <= tol).all(), np.abs(a64 - b64).max()
+        ref = oracle.corr_fwd(gmap.double().cpu().numpy(), pyr[l].double().cpu().numpy(),
+                              (coords / s).cpu().numpy()[:, sel], kk1.cpu().numpy()[sel],
+                              jj1.cpu().numpy()[sel], 3)
+        _close_f16(a64[:, sel], ref)
