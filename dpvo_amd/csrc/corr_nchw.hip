@@ -12,8 +12,11 @@
 // straight from HBM.  Each wave (one edge, one level):
 //   * loads the box 32 channels at a time: per channel, bh rows x npr aligned
 //     pieces of G halves (16-B pieces when W2 % 8 == 0, 8-B when W2 % 4 == 0);
-//     lane = (channel cl = lane & 31, row parity hf = lane >> 5), so the
-//     per-piece address is one lane base plus a wave-uniform offset;
+//     one load instruction takes the whole box of 2 channels (16-B pieces) or
+//     1 channel (8-B pieces), lane = (channel, row, piece): the lines a box
+//     row needs are shared by the lanes of the row.  (Lane = (channel, row
+//     parity), every lane on its own 128-B line, made the level-1 call 1.6x
+//     slower: the line requests, not the bytes, bound the load path);
 //   * writes them to an LDS image [32 channels][P pixels], P = bh x Wp
 //     (Wp = npr x G) padded to an ODD number of 16-pixel tiles;
 //   * reads B fragments with ds_read_b64_tr_b16 (gfx950's transposing LDS
@@ -92,18 +95,115 @@ __device__ __forceinline__ X nc_sel(int l, X a, X b, X c, X d) {
   return l == 0 ? a : l == 1 ? b : l == 2 ? c : d;
 }
 
-// One edge at one level.  G = piece width in halves (8 or 4).
+// The matrix-core part of one edge at one level: G[k][px] for every image
+// pixel into Gs (np rows of P floats).  G = piece width in halves.
 template <int G>
+__device__ __forceinline__ void nc_fast(const __half* __restrict__ fmap1,
+                                        const __half* __restrict__ f2lvl, int H2, int W2, int b,
+                                        int ix, int jx, int np, int N1, int N2, int ylo, int bh,
+                                        int xs, int npr, int Wp, int nt, char* wlds) {
+  // a load instruction covers the whole box (bh rows x npr pieces) of kCh
+  // channels: lane (ch = lane / kLc, piece idx = lane % kLc -> row idx / npr,
+  // piece idx % npr); a 32-channel chunk is kIns instructions (64 VGPRs)
+  constexpr int kCh = G == 8 ? 2 : 1, kLc = kWave / kCh, kIns = kNcChunk / kCh;
+  using PT = typename NcPiece<G>::type;
+  const int lane = threadIdx.x & (kWave - 1);
+  float* Gs = reinterpret_cast<float*>(wlds);
+  const int P = nt * 16;
+  const size_t HW2 = (size_t)H2 * W2;
+  const __half* f2 = f2lvl + ((size_t)b * N2 + jx) * kNcC * HW2;
+  const __half* f1 = fmap1 + ((size_t)b * N1 + ix) * kNcC * np;
+  // per-lane piece (fixed for every chunk and instruction): an instruction
+  // then touches kCh x bh x (1-2) 128-B lines, not one line per lane
+  const int pidx = lane % kLc, pch = lane / kLc;
+  const bool pv = pidx < bh * npr;
+  const int prow = pv ? pidx / npr : 0, ppc = pv ? pidx - prow * npr : 0;
+  const __half* src0 = f2 + (size_t)pch * HW2 + (size_t)(ylo + prow) * W2 + xs + ppc * G;
+  PT buf[kIns];
+  auto issue = [&](int u) __attribute__((always_inline)) {
+    if (pv) {
+      const __half* su = src0 + (size_t)u * kNcChunk * HW2;
+#pragma unroll
+      for (int i = 0; i < kIns; i++) buf[i] = ldg<PT>(su + (size_t)(kCh * i) * HW2);
+    }
+  };
+  char* wb = wlds + (pch * P + prow * Wp + ppc * G) * 2;  // the lane's piece in channel row 0
+  auto stage = [&]() __attribute__((always_inline)) {
+    if (pv) {
+#pragma unroll
+      for (int i = 0; i < kIns; i++) *reinterpret_cast<PT*>(wb + kCh * i * P * 2) = buf[i];
+    }
+  };
+
+  // gmap patch [C][np] (16-B units, C * np * 2 is a multiple of 16) -> LDS
+  // -> A fragments; its loads overlap chunk 0's
+  constexpr int kRA = (kNcC * kNcNpMax / 8 + kWave - 1) / kWave;
+  const int n16 = kNcC * np / 8;
+  u4 pa[kRA];
+#pragma unroll
+  for (int r = 0; r < kRA; r++) pa[r] = ldg<u4>(f1 + 8 * min(lane + kWave * r, n16 - 1));
+  issue(0);
+#pragma unroll
+  for (int r = 0; r < kRA; r++)
+    if (lane + kWave * r < n16) reinterpret_cast<u4*>(wlds)[lane + kWave * r] = pa[r];
+  wave_lds_sync();
+  const int g4 = lane >> 4, am = lane & 15;
+  h8 A[kNcChunks];
+  {
+    const _Float16* ph = reinterpret_cast<const _Float16*>(wlds);
+    const bool arow = am < np;
+#pragma unroll
+    for (int u = 0; u < kNcChunks; u++)
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int c = kNcChunk * u + (j < 4 ? 4 * g4 + j : 16 + 4 * g4 + j - 4);
+        A[u][j] = arow ? ph[c * np + am] : (_Float16)0.0f;
+      }
+  }
+  wave_lds_sync();  // patch read: the image may overwrite it
+
+  // transposed-read address of lane (g4, row q' = (lane >> 2) & 3, col 4 (lane & 3))
+  const char* ta = wlds + ((4 * g4 + ((lane >> 2) & 3)) * P + 4 * (lane & 3)) * 2;
+  const int ta1 = 16 * P * 2;  // the second read: channel rows 16 + 4 g4 + q'
+  f4 acc[kNcMaxTiles];
+#pragma unroll
+  for (int t = 0; t < kNcMaxTiles; t++) acc[t] = (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < kNcChunks; u++) {
+    stage();
+    wave_lds_sync();
+    if (u + 1 < kNcChunks) issue(u + 1);
+#pragma unroll
+    for (int t = 0; t < kNcMaxTiles; t++) {
+      if (t < nt) {
+        const h4 b0 = tr_read(ta + 32 * t), b1 = tr_read(ta + ta1 + 32 * t);
+        const h8 bb = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[u], bb, acc[t], 0, 0, 0);
+      }
+    }
+    wave_lds_sync();  // this chunk's reads before the next chunk's writes
+  }
+  // D tile t: lane (col n = lane & 15, rows 4 g4 + r) -> G[k][16 t + n]
+#pragma unroll
+  for (int t = 0; t < kNcMaxTiles; t++) {
+    if (t < nt) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int k = 4 * g4 + r;
+        if (k < np) Gs[k * P + 16 * t + am] = acc[t][r];
+      }
+    }
+  }
+}
+
+// One edge at one level; g = the level's widest piece (8 or 4 halves).
 __device__ __forceinline__ void nc_edge(const __half* __restrict__ fmap1,
-                                        const __half* __restrict__ f2lvl, int H2, int W2,
+                                        const __half* __restrict__ f2lvl, int H2, int W2, int g,
                                         float scale, bool use_scale,
                                         const float* __restrict__ coords, int b, int m, int ix,
                                         int jx, int M, int np, int N1, int N2, int R, char* wlds,
                                         __half* __restrict__ out_t, float* __restrict__ out_f,
                                         int out_stride, int out_off) {
-  // pieces per lane per chunk: row pairs x pieces per row (18 x 16 B or 35 x 8 B)
-  constexpr int kNpr = G == 8 ? 3 : 5, kRows2 = G == 8 ? 6 : 7;
-  using PT = typename NcPiece<G>::type;
   const int lane = threadIdx.x & (kWave - 1);
   const int D = 2 * R + 2, Dp = D - 1;
   float* Gs = reinterpret_cast<float*>(wlds);
@@ -135,111 +235,30 @@ __device__ __forceinline__ void nc_edge(const __half* __restrict__ fmap1,
   int bw = xhi - xlo + 1, bh = yhi - ylo + 1;
   if (bw <= 0 || bh <= 0 || !idx_ok) bw = bh = 0;
   const int npx = bw * bh;
-  // image geometry: rows start at the G-aligned column xs <= xlo
-  const int xs = xlo & ~(G - 1);
-  const int npr = npx > 0 ? (xhi - xs) / G + 1 : 0;  // pieces per box row
-  const int Wp = npr * G;
-  const int nt = ((bh * Wp + 15) >> 4) | 1;  // odd tile count (bank-conflict-free reads)
-  const int rows2 = (bh + 1) >> 1;          // row pairs
-  const bool fast = npx > 0 && nt <= kNcMaxTiles && rows2 <= kRows2 && npr <= kNpr;
+  // image geometry: rows start at the G-aligned column xs <= xlo; 16-B pieces
+  // where the level allows them and the box fits one 2-channel instruction,
+  // else 8-B pieces (one channel per instruction), else the raw path
+  int xs = 0, npr = 0, Wp = 0, nt = 1, Gsel = 0;
+  auto fits = [&](int G, int lanes) {
+    xs = xlo & ~(G - 1);
+    npr = (xhi - xs) / G + 1;  // pieces per box row
+    Wp = npr * G;
+    nt = ((bh * Wp + 15) >> 4) | 1;  // odd tile count (bank-conflict-free reads)
+    return nt <= kNcMaxTiles && bh * npr <= lanes;
+  };
+  if (npx > 0) {
+    if (g == 8 && fits(8, kWave / 2)) Gsel = 8;
+    else if (fits(4, kWave)) Gsel = 4;
+  }
+  const bool fast = Gsel != 0;
   const int P = nt * 16;
   const int xoff = xlo - xs;
   const size_t HW2 = (size_t)H2 * W2;
 
-  if (fast) {
-    const __half* f2 = f2lvl + ((size_t)b * N2 + jx) * kNcC * HW2;
-    const __half* f1 = fmap1 + ((size_t)b * N1 + ix) * kNcC * np;
-    const int cl = lane & 31, hf = lane >> 5;
-    const __half* src0 = f2 + (size_t)cl * HW2 + (size_t)ylo * W2 + xs;
-    PT buf[kRows2 * kNpr];
-    // chunk u's pieces: lane (cl, hf) loads channel 32u + cl, box rows
-    // hf + 2 r2 (an odd box height's last hf = 1 row re-reads the row above:
-    // loaded, not written), pieces pc of G halves.  Row and piece loops are
-    // compile-time (per-piece offsets: one scalar per row pair + immediates)
-    auto issue = [&](int u) __attribute__((always_inline)) {
-      const __half* s = src0 + (size_t)u * kNcChunk * HW2;
-#pragma unroll
-      for (int r2 = 0; r2 < kRows2; r2++) {
-        if (r2 < rows2) {
-          const __half* sr = s + (size_t)(2 * r2 + (hf && 2 * r2 + 1 < bh ? 1 : 0)) * W2;
-#pragma unroll
-          for (int pc = 0; pc < kNpr; pc++)
-            if (pc < npr) buf[r2 * kNpr + pc] = ldg<PT>(sr + pc * G);
-        }
-      }
-    };
-    char* wb = wlds + (cl * P + hf * Wp) * 2;  // the lane's first piece in the image
-    auto stage = [&]() __attribute__((always_inline)) {
-#pragma unroll
-      for (int r2 = 0; r2 < kRows2; r2++) {
-        if (r2 < rows2 && hf + 2 * r2 < bh) {
-#pragma unroll
-          for (int pc = 0; pc < kNpr; pc++)
-            if (pc < npr)
-              *reinterpret_cast<PT*>(wb + (2 * r2 * Wp + pc * G) * 2) = buf[r2 * kNpr + pc];
-        }
-      }
-    };
-
-    // gmap patch [C][np] (16-B units, C * np * 2 is a multiple of 16) -> LDS
-    // -> A fragments; its loads overlap chunk 0's
-    constexpr int kRA = (kNcC * kNcNpMax / 8 + kWave - 1) / kWave;
-    const int n16 = kNcC * np / 8;
-    u4 pa[kRA];
-#pragma unroll
-    for (int r = 0; r < kRA; r++) pa[r] = ldg<u4>(f1 + 8 * min(lane + kWave * r, n16 - 1));
-    issue(0);
-#pragma unroll
-    for (int r = 0; r < kRA; r++)
-      if (lane + kWave * r < n16) reinterpret_cast<u4*>(wlds)[lane + kWave * r] = pa[r];
-    wave_lds_sync();
-    const int g4 = lane >> 4, am = lane & 15;
-    h8 A[kNcChunks];
-    {
-      const _Float16* ph = reinterpret_cast<const _Float16*>(wlds);
-      const bool arow = am < np;
-#pragma unroll
-      for (int u = 0; u < kNcChunks; u++)
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const int c = kNcChunk * u + (j < 4 ? 4 * g4 + j : 16 + 4 * g4 + j - 4);
-          A[u][j] = arow ? ph[c * np + am] : (_Float16)0.0f;
-        }
-    }
-    wave_lds_sync();  // patch read: the image may overwrite it
-
-    // transposed-read address of lane (g4, row q' = (lane >> 2) & 3, col 4 (lane & 3))
-    const char* ta = wlds + ((4 * g4 + ((lane >> 2) & 3)) * P + 4 * (lane & 3)) * 2;
-    const int ta1 = 16 * P * 2;  // the second read: channel rows 16 + 4 g4 + q'
-    f4 acc[kNcMaxTiles];
-#pragma unroll
-    for (int t = 0; t < kNcMaxTiles; t++) acc[t] = (f4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < kNcChunks; u++) {
-      stage();
-      wave_lds_sync();
-      if (u + 1 < kNcChunks) issue(u + 1);
-#pragma unroll
-      for (int t = 0; t < kNcMaxTiles; t++) {
-        if (t < nt) {
-          const h4 b0 = tr_read(ta + 32 * t), b1 = tr_read(ta + ta1 + 32 * t);
-          const h8 bb = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[u], bb, acc[t], 0, 0, 0);
-        }
-      }
-      wave_lds_sync();  // this chunk's reads before the next chunk's writes
-    }
-    // D tile t: lane (col n = lane & 15, rows 4 g4 + r) -> G[k][16 t + n]
-#pragma unroll
-    for (int t = 0; t < kNcMaxTiles; t++) {
-      if (t < nt) {
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int k = 4 * g4 + r;
-          if (k < np) Gs[k * P + 16 * t + am] = acc[t][r];
-        }
-      }
-    }
+  if (Gsel == 8) {
+    nc_fast<8>(fmap1, f2lvl, H2, W2, b, ix, jx, np, N1, N2, ylo, bh, xs, npr, Wp, nt, wlds);
+  } else if (Gsel == 4) {
+    nc_fast<4>(fmap1, f2lvl, H2, W2, b, ix, jx, np, N1, N2, ylo, bh, xs, npr, Wp, nt, wlds);
   } else if (npx > 0) {
     // ---- rare: windows too spread for the image; raw[k][yy][xx] directly ----
     const __half* f2 = f2lvl + ((size_t)b * N2 + jx) * kNcC * HW2;
@@ -295,16 +314,125 @@ __device__ __forceinline__ void nc_edge(const __half* __restrict__ fmap1,
   wave_lds_sync();
 }
 
+// ---- XCD-aware edge order, computed by every workgroup (no extra launch) ----
+// Workgroups run on XCD blockIdx.x % 8 (round-robin dispatch, gridDim.x a
+// multiple of 8).  XCD x takes the x-th eighth of the edges sorted by target
+// frame (stable counting sort of jj), so the 128-B lines of a frame's channel
+// planes are fetched into one XCD's L2 instead of every XCD's: an NCHW box row
+// uses ~20 B of each line it touches, so re-fetching lines, not bytes, bounds
+// the level-1 call (cfg2: 51 -> 28 us, scripts/nchw_order_probe.py).  The
+// workgroup's chunk c holds sorted positions 4c .. 4c+3; thread t counts the
+// edges of its contiguous slice of jj per target bin, a block scan of the
+// counts gives the rank of every match, and the owner of each wanted rank
+// writes its edge id.  Edge ids are a bijection of positions, so the results
+// are those of the unordered launch (every edge writes only its own output).
+constexpr int kOrdMaxE = 16384, kOrdMaxN2 = 2048;
+
+__device__ __forceinline__ int ord_bin(int64_t v, int N2) {
+  return (v >= 0 && v < N2) ? (int)v : N2;  // out-of-range indices: one last bin
+}
+
+// LDS scratch (the waves' areas, before any image): bin of every edge u16 [M],
+// hist [N2 + 2] ints, wave totals, the wanted (bin, rank) pairs; sel [4] is
+// outside the waves' areas (read after the last barrier)
+__device__ __forceinline__ void nc_order(const int64_t* __restrict__ jj, int M, int N2, int c,
+                                         char* smem, int* sel) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int T = kNcWaves * kWave;
+  const int nb = N2 + 1;
+  unsigned short* ebin = reinterpret_cast<unsigned short*>(smem);  // [M]
+  int* hist = reinterpret_cast<int*>(smem + 2 * ((M + 7) & ~7));   // [nb + 1]: counts -> starts
+  int2* wtot = reinterpret_cast<int2*>(hist + ((nb + 2) & ~1));    // [kNcWaves]
+  int* want = reinterpret_cast<int*>(wtot + kNcWaves);             // [8]
+  for (int v = tid; v <= nb; v += T) hist[v] = 0;
+  __syncthreads();
+  for (int e = tid; e < M; e += T) {
+    const int v = ord_bin(jj[e], N2);
+    ebin[e] = (unsigned short)v;
+    atomicAdd(&hist[v], 1);
+  }
+  __syncthreads();
+  if (wid == 0) {  // exclusive scan of the bins by one wave, 64 at a time
+    int carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += kWave) {
+      const int bb = b0 + lane, v = bb < nb ? hist[bb] : 0;
+      const int inc = wave_incl_sum(v);
+      if (bb < nb) hist[bb] = carry + inc - v;
+      carry += __builtin_amdgcn_readlane(inc, 63);
+    }
+    if (lane == 0) hist[nb] = carry;
+  }
+  __syncthreads();
+  if (tid < kNcWaves) {  // bin and rank of position 4c + tid (binary search of the starts)
+    const int p = 4 * c + tid;
+    int lo = 0, hi = nb;  // largest b with start[b] <= p
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (hist[mid] <= p) lo = mid; else hi = mid;
+    }
+    want[2 * tid] = p < M ? lo : -1;
+    want[2 * tid + 1] = p - hist[lo];
+  }
+  __syncthreads();
+  int wb[kNcWaves];
+#pragma unroll
+  for (int w = 0; w < kNcWaves; w++) wb[w] = want[2 * w];
+  // this thread's contiguous slice of the edges (rank = slices before + order
+  // inside): matches of the 4 wanted bins, packed 16 bits each (<= M < 2^16)
+  const int K = (M + T - 1) / T, e0 = min(tid * K, M), e1 = min(e0 + K, M);
+  int c01 = 0, c23 = 0;
+  for (int e = e0; e < e1; e++) {
+    const int v = ebin[e];
+    c01 += (v == wb[0] ? 1 : 0) + (v == wb[1] ? 1 << 16 : 0);
+    c23 += (v == wb[2] ? 1 : 0) + (v == wb[3] ? 1 << 16 : 0);
+  }
+  const int i01 = wave_incl_sum(c01), i23 = wave_incl_sum(c23);
+  if (lane == 63) wtot[wid] = make_int2(i01, i23);
+  __syncthreads();
+  int x01 = i01 - c01, x23 = i23 - c23;  // exclusive prefix over the block
+  for (int w = 0; w < wid; w++) {
+    x01 += wtot[w].x;
+    x23 += wtot[w].y;
+  }
+#pragma unroll
+  for (int w = 0; w < kNcWaves; w++) {
+    const int pre = ((w < 2 ? x01 : x23) >> (16 * (w & 1))) & 0xffff;
+    const int cnt = ((w < 2 ? c01 : c23) >> (16 * (w & 1))) & 0xffff;
+    const int r = want[2 * w + 1];
+    if (wb[w] >= 0 && r >= pre && r < pre + cnt) {  // exactly one thread
+      int seen = pre;
+      for (int e = e0; e < e1; e++)
+        if (ebin[e] == wb[w]) {
+          if (seen == r) sel[w] = e;
+          ++seen;
+        }
+    }
+    if (wb[w] < 0 && tid == 0) sel[w] = -1;
+  }
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(kNcWaves* kWave, 2)  // 2 workgroups (8 waves) per CU
     corr_nchw_kernel(const __half* __restrict__ fmap1, NcLevels lv, int use_scale,
                      const float* __restrict__ coords, const int64_t* __restrict__ ii,
                      const int64_t* __restrict__ jj, int B, int M, int np, int N1, int N2, int R,
-                     int L, __half* __restrict__ out_t, float* __restrict__ out_f) {
+                     int L, int ordered, __half* __restrict__ out_t, float* __restrict__ out_f) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wid = wave_uniform(threadIdx.x / kWave);
   char* wlds = smem + wid * kNcWaveBytes;
-  const int unit = blockIdx.x * kNcWaves + wid;
-  if (unit >= B * M) return;  // waves are independent: no block barrier below
+  int unit;
+  if (ordered) {  // B == 1
+    int* sel = reinterpret_cast<int*>(smem + kNcWaves * kNcWaveBytes);
+    const int nwg = (M + kNcWaves - 1) / kNcWaves, per = (nwg + 7) / 8;
+    const int c = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (c >= nwg) return;  // workgroup-uniform
+    nc_order(jj, M, N2, c, smem, sel);
+    unit = wave_uniform(sel[wid]);
+    if (unit < 0) return;
+  } else {
+    unit = blockIdx.x * kNcWaves + wid;
+    if (unit >= B * M) return;  // waves are independent: no block barrier below
+  }
   const int l = blockIdx.y;
   const int b = unit / M, m = unit % M;
   const int ix = wave_uniform((int)ii[m]), jx = wave_uniform((int)jj[m]);
@@ -313,12 +441,8 @@ __global__ void __launch_bounds__(kNcWaves* kWave, 2)  // 2 workgroups (8 waves)
   const int W2 = nc_sel(l, lv.W2[0], lv.W2[1], lv.W2[2], lv.W2[3]);
   const int g = nc_sel(l, lv.g[0], lv.g[1], lv.g[2], lv.g[3]);
   const float s = nc_sel(l, lv.scale[0], lv.scale[1], lv.scale[2], lv.scale[3]);
-  if (g == 8)
-    nc_edge<8>(fmap1, f2, H2, W2, s, use_scale != 0, coords, b, m, ix, jx, M, np, N1, N2, R, wlds,
-               out_t, out_f, L, l);
-  else
-    nc_edge<4>(fmap1, f2, H2, W2, s, use_scale != 0, coords, b, m, ix, jx, M, np, N1, N2, R, wlds,
-               out_t, out_f, L, l);
+  nc_edge(fmap1, f2, H2, W2, g, s, use_scale != 0, coords, b, m, ix, jx, M, np, N1, N2, R, wlds,
+          out_t, out_f, L, l);
 }
 
 }  // namespace
@@ -350,21 +474,34 @@ int corr_nchw_mma(const void* fmap1, const void* const* fmap2, const int* H2, co
     lv.scale[l] = scale ? scale[l] : 1.0f;
   }
   if ((long long)B * M == 0) return DPVO_OK;
-  static bool attr = false;  // 4 x 17.7 KB per workgroup: above the default 64 KB
+  static bool attr = false;  // 4 x 17.7 KB per workgroup (+ the order's 4 edge ids): above 64 KB
   if (!attr) {
     if (hipFuncSetAttribute((const void*)corr_nchw_kernel,
                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                            kNcWaves * kNcWaveBytes) != hipSuccess) {
+                            kNcWaves * kNcWaveBytes + 16) != hipSuccess) {
       (void)hipGetLastError();  // not sticky: report it here, not at a later launch
       return DPVO_ERR_LAUNCH;
     }
     attr = true;
   }
-  const dim3 grid((unsigned)(((long long)B * M + kNcWaves - 1) / kNcWaves), L),
-      block(kNcWaves * kWave);
-  hipLaunchKernelGGL(corr_nchw_kernel, grid, block, (size_t)kNcWaves * kNcWaveBytes, s,
+  // XCD-aware order for a single batch of a DPVO-sized graph, when some level's
+  // ring is larger than the L2s together (8 x 4 MB): the order's prologue costs
+  // ~6 us per workgroup and pays only where lines are re-fetched from the
+  // Infinity Cache / HBM (cfg2 level 1, 177 MB: 51 -> 31 us; level 4, 11 MB:
+  // 21 -> 23 us)
+  size_t ring = 0;
+  for (int l = 0; l < L; l++) {
+    const size_t r = (size_t)N2 * kNcC * H2[l] * W2[l] * 2;
+    ring = r > ring ? r : ring;
+  }
+  const int ordered = B == 1 && M <= kOrdMaxE && N2 >= 1 && N2 <= kOrdMaxN2 &&
+                      ring > ((size_t)32 << 20);
+  unsigned gx = (unsigned)(((long long)B * M + kNcWaves - 1) / kNcWaves);
+  if (ordered) gx = 8u * ((gx + 7u) / 8u);
+  const dim3 grid(gx, L), block(kNcWaves * kWave);
+  hipLaunchKernelGGL(corr_nchw_kernel, grid, block, (size_t)kNcWaves * kNcWaveBytes + 16, s,
                      (const __half*)fmap1, lv, use_scale ? 1 : 0, coords, ii, jj, B, M, np, N1,
-                     N2, R, L, (__half*)out_t, out_f);
+                     N2, R, L, ordered, (__half*)out_t, out_f);
   return launch_status();
 }
 
