@@ -14,6 +14,9 @@
 #include <vector>
 
 #include "ba_solve.hpp"
+#ifdef WSOLVE_MMA
+#include "ba_gj_mma.hpp"
+#endif
 
 using namespace dpvo::bad;
 
@@ -37,8 +40,29 @@ __global__ void __launch_bounds__(256) k_wsolve(const double* S, const double* y
   for (int k = threadIdx.x; k < 36 * NB; k += blockDim.x) Sd[k] = S[k];
   for (int k = threadIdx.x; k < n; k += blockDim.x) yd[k] = y[k];
   __syncthreads();
+#ifdef WSOLVE_MMA
+  // the sweep solver's workspace after S, y, x (16-B aligned)
+  GJSolve g;
+  g.S = Sd;
+  g.y = yd;
+  g.x = s.x;
+  const int np = gj_np(N);
+  {  // 16-B aligned by pointer arithmetic (an integer round trip loses the LDS
+     // address space: every access would become a flat load)
+    char* p = reinterpret_cast<char*>(s.r + n);
+    p += (16 - (int)(reinterpret_cast<uintptr_t>(p) & 15)) & 15;
+    g.Mi = reinterpret_cast<float*>(p);
+  }
+  g.C = g.Mi + np * np;
+  g.V = g.C + 8 * np;
+  g.W = g.V + 8 * np;
+  g.v = g.W + 8 * np;
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  const bool ok = wsolve_mma(g, N, refine, &f, stl);
+#else
   const long long t0 = __builtin_amdgcn_s_memtime();
   const bool ok = wsolve(s, N, refine, &f, stl);
+#endif
   const long long t1 = __builtin_amdgcn_s_memtime();
   for (int k = threadIdx.x; k < n; k += blockDim.x) dX[k] = s.x[k];
   for (int k = threadIdx.x; k < 64; k += blockDim.x) stg[k] = stl[k];
@@ -109,7 +133,11 @@ int main(int argc, char** argv) {
   hipMalloc(&dfail, sizeof(int));
   hipMemcpy(dS, Sb.data(), sizeof(double) * Sb.size(), hipMemcpyHostToDevice);
   hipMemcpy(dy, y.data(), sizeof(double) * n, hipMemcpyHostToDevice);
-  const size_t lds = sizeof(double) * (36 * NB + 3 * n) + wsolve_bytes(N);
+  const size_t lds = sizeof(double) * (36 * NB + 3 * n) + wsolve_bytes(N) + 64
+#ifdef WSOLVE_MMA
+                     + gj_bytes(N)
+#endif
+      ;
   hipFuncSetAttribute((const void*)k_wsolve, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   std::vector<long long> cs;
   for (int r = 0; r < 40; r++) {
@@ -122,6 +150,15 @@ int main(int argc, char** argv) {
   std::sort(cs.begin(), cs.end());
   long long h[64];
   hipMemcpy(h, dst, sizeof(h), hipMemcpyDeviceToHost);
+#ifdef WSOLVE_MMA
+  printf("load %lld |", h[1] - h[0]);
+  for (int k = 0; k < N; k++) printf(" %lld", h[2 + k] - h[1 + k]);
+  printf(" | store %lld | solve %lld", h[40] - h[1 + N], h[41] - h[40]);
+  printf(" | k2: publish+bar %lld rows %lld bar %lld mfma %lld fix %lld", h[50] - h[3], h[51] - h[50],
+         h[52] - h[51], h[53] - h[52], h[4] - h[53]);
+  for (int it = 0; it < refine; it++) printf(" ref%d %lld", it, h[42 + it] - h[41 + it]);
+  printf("\n");
+#else
   printf("pre %lld piv0 %lld |", h[1] - h[0], 0LL);
   for (int k = 0; k < N; k++) printf(" %lld", h[2 + k] - (k ? h[1 + k] : h[1]));
   printf(" | post %lld | solve %lld", h[40] - h[1 + N], h[41] - h[40]);
@@ -133,6 +170,7 @@ int main(int argc, char** argv) {
 #endif
   for (int it = 0; it < refine; it++) printf(" ref%d %lld", it, h[42 + it] - (it ? h[41 + it] : h[41]));
   printf("\n");
+#endif
   std::vector<double> got(n);
   int fail = 0;
   hipMemcpy(got.data(), dX, sizeof(double) * n, hipMemcpyDeviceToHost);
