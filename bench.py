@@ -546,6 +546,13 @@ def main():
             },
             "roofline": {
                 "kernel": "corr_nhwc_kernel (A-CORR, all levels, one launch)",
+                # how the fp32 products are formed
+                "products": ("fp32 features: a*b = ah*bh + ah*bl + (al*bh)*2^-11 from f16 "
+                             "pieces on v_mfma_f32_16x16x32_f16, fp32 accumulation "
+                             "(per-product error <= ~2^-21|a||b| + 2^-25|a|); "
+                             "non-finite levels redone in plain fp32"
+                             if args.features == "f32" else
+                             "fp16 x fp16 on v_mfma_f32_16x16x32_f16, fp32 accumulation"),
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
