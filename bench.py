@@ -38,7 +38,7 @@ sys.path.insert(0, REPO)
 METRIC = "update-iterations/sec (altcorr+fastba) on 96-patch/2048-edge graph, 1→8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                            "profiles", "r04_corr_traffic.json")
+                            "profiles", "r05_corr_traffic.json")
 
 
 def pmc_traffic(config):
