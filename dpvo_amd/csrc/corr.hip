@@ -19,7 +19,7 @@
 
 namespace dpvo {
 
-// corr_nchw.hip: the matrix-core forward for NCHW fp16 levels (returns
+// corr_nchw.hip: the matrix-core forward for NCHW fp16 / fp32 levels (returns
 // DPVO_ERR_UNSUPPORTED outside its shape; the VALU kernels below take those)
 int corr_nchw_mma(const void* fmap1, const void* const* fmap2, const int* H2, const int* W2,
                   const float* scale, int L, bool use_scale, const float* coords,
@@ -529,7 +529,7 @@ DPVO_EXPORT int dpvo_corr_forward(const void* fmap1, const void* fmap2, const fl
   if (!fmap1 || !fmap2 || !coords || !ii || !jj || !out) return DPVO_ERR_INVALID;
   hipStream_t s = as_stream(stream);
   const int np = H * W;
-  if (dtype == DPVO_F16) {
+  if (dtype == DPVO_F16 || dtype == DPVO_F32) {
     const int st = corr_nchw_mma(fmap1, &fmap2, &H2, &W2, nullptr, 1, false, coords, ii, jj, B,
                                  M, C, np, N1, N2, radius, dtype, out, nullptr, s);
     if (st != DPVO_ERR_UNSUPPORTED) return st;
@@ -565,7 +565,7 @@ DPVO_EXPORT int dpvo_corr_forward_levels(const void* fmap1, const void* const* f
   }
   hipStream_t s = as_stream(stream);
   const int np = H * W;
-  if (dtype == DPVO_F16) {
+  if (dtype == DPVO_F16 || dtype == DPVO_F32) {
     const int st = corr_nchw_mma(fmap1, fmap2, H2, W2, scale, L, true, coords, ii, jj, B, M, C,
                                  np, N1, N2, radius, dtype, nullptr, out, s);
     if (st != DPVO_ERR_UNSUPPORTED) return st;

@@ -1,6 +1,6 @@
-// corr_nchw.hip -- A-CORR on the matrix cores for NCHW fp16 feature maps: the
-// layout DPVO allocates (dpvo.py:111-112, fp16 under its default
-// MIXED_PRECISION runtime), behind the unchanged per-level entry
+// corr_nchw.hip -- A-CORR on the matrix cores for NCHW feature maps (fp16 and
+// fp32): the layout DPVO allocates (dpvo.py:111-112, fp16 under its default
+// MIXED_PRECISION runtime, fp32 without it), behind the unchanged per-level entry
 // (correlation.cpp:32-38 -> cuda_corr.forward, called per level at
 // dpvo.py:462-465) and the fused multi-level one.
 //
@@ -33,6 +33,10 @@
 // element j of its fragment, channel 32u + 4g + j (j < 4) or 32u + 16 + 4g +
 // j - 4 (j >= 4) -- the rows of its two transposed reads -- in both the A
 // (gmap patch) and the B (box) fragment.
+// fp32 features: the same image holds 16 channels (the same bytes), B comes
+// back with plain ds_read_b32 (lane (n, q): channel 4s + q, pixel n) and
+// v_mfma_f32_16x16x4_f32 forms exact fp32 products (K step s: channels
+// 16u + 4s .. + 3); 8 chunks per level.
 #include "common.hpp"
 
 namespace dpvo {
@@ -40,19 +44,18 @@ namespace {
 
 constexpr int kNcWaves = 4;      // edges per workgroup
 constexpr int kNcC = 128;        // channels (DPVO fmap width)
-constexpr int kNcChunk = 32;     // channels per LDS image (one MFMA K step)
-constexpr int kNcChunks = kNcC / kNcChunk;
+constexpr int kNcImgElemBytes = 64;  // channels per LDS image x element bytes
 constexpr int kNcMaxTiles = 17;  // odd; box image <= 272 px
 constexpr int kNcMaxPx = 16 * kNcMaxTiles;
 constexpr int kNcNpMax = 16;     // p * p <= 16 (one MFMA row tile)
 constexpr int kNcMaxL = 4;
-// per wave: the image (reused as G: np x P floats <= 16 x 272, or the slow
-// path's np x D x D <= 16 x 256) + the patch geometry
-constexpr int kNcImgBytes = kNcChunk * kNcMaxPx * 2;
+// per wave: the image (32 fp16 / 16 fp32 channels x P; reused as G: np x P
+// floats <= 16 x 272, or the slow path's np x D x D <= 16 x 256) + geometry
+constexpr int kNcImgBytes = kNcImgElemBytes * kNcMaxPx;
 
 struct NcLevels {
-  const __half* f2[kNcMaxL];  // [B, N2, C, H2, W2]
-  int H2[kNcMaxL], W2[kNcMaxL], g[kNcMaxL];
+  const void* f2[kNcMaxL];  // [B, N2, C, H2, W2] (__half or float)
+  int H2[kNcMaxL], W2[kNcMaxL], pb[kNcMaxL];  // pb: widest piece in bytes (16 or 8)
   float scale[kNcMaxL];
 };
 
@@ -70,12 +73,12 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef unsigned u2 __attribute__((ext_vector_type(2)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
-template <int G>
+template <int PB>
 struct NcPiece;
 template <>
-struct NcPiece<8> { typedef u4 type; };  // 16 B
+struct NcPiece<16> { typedef u4 type; };
 template <>
-struct NcPiece<4> { typedef u2 type; };  // 8 B
+struct NcPiece<8> { typedef u2 type; };
 
 // global-address-space load (a generic pointer would be a flat load, counted
 // in both vmcnt and lgkmcnt)
@@ -96,89 +99,117 @@ __device__ __forceinline__ X nc_sel(int l, X a, X b, X c, X d) {
 }
 
 // The matrix-core part of one edge at one level: G[k][px] for every image
-// pixel into Gs (np rows of P floats).  G = piece width in halves.
-template <int G>
-__device__ __forceinline__ void nc_fast(const __half* __restrict__ fmap1,
-                                        const __half* __restrict__ f2lvl, int H2, int W2, int b,
-                                        int ix, int jx, int np, int N1, int N2, int ylo, int bh,
-                                        int xs, int npr, int Wp, int nt, char* wlds) {
-  // a load instruction covers the whole box (bh rows x npr pieces) of kCh
-  // channels: lane (ch = lane / kLc, piece idx = lane % kLc -> row idx / npr,
-  // piece idx % npr); a 32-channel chunk is kIns instructions (64 VGPRs)
-  constexpr int kCh = G == 8 ? 2 : 1, kLc = kWave / kCh, kIns = kNcChunk / kCh;
-  using PT = typename NcPiece<G>::type;
+// pixel into Gs (np rows of P floats).  T: __half or float; PB: piece bytes
+// (16 or 8); CH: channels per load instruction (2: the box fits 32 lanes).
+template <typename T, int PB, int CH>
+__device__ __forceinline__ void nc_fast(const T* __restrict__ fmap1, const T* __restrict__ f2lvl,
+                                        int H2, int W2, int b, int ix, int jx, int np, int N1,
+                                        int N2, int ylo, int bh, int xs, int npr, int Wp, int nt,
+                                        char* wlds) {
+  constexpr bool kHalf = std::is_same<T, __half>::value;
+  constexpr int G = PB / (int)sizeof(T);                 // elements per piece
+  constexpr int KC = kNcImgElemBytes / (int)sizeof(T);   // channels per image (32 / 16)
+  constexpr int kChunks = kNcC / KC;
+  constexpr int kLc = kWave / CH, kIns = KC / CH;        // lanes per channel, loads per chunk
+  using PT = typename NcPiece<PB>::type;
   const int lane = threadIdx.x & (kWave - 1);
   float* Gs = reinterpret_cast<float*>(wlds);
   const int P = nt * 16;
   const size_t HW2 = (size_t)H2 * W2;
-  const __half* f2 = f2lvl + ((size_t)b * N2 + jx) * kNcC * HW2;
-  const __half* f1 = fmap1 + ((size_t)b * N1 + ix) * kNcC * np;
+  const T* f2 = f2lvl + ((size_t)b * N2 + jx) * kNcC * HW2;
+  const T* f1 = fmap1 + ((size_t)b * N1 + ix) * kNcC * np;
   // per-lane piece (fixed for every chunk and instruction): an instruction
-  // then touches kCh x bh x (1-2) 128-B lines, not one line per lane
+  // then touches CH x bh x (1-2) 128-B lines, not one line per lane
   const int pidx = lane % kLc, pch = lane / kLc;
   const bool pv = pidx < bh * npr;
   const int prow = pv ? pidx / npr : 0, ppc = pv ? pidx - prow * npr : 0;
-  const __half* src0 = f2 + (size_t)pch * HW2 + (size_t)(ylo + prow) * W2 + xs + ppc * G;
+  const T* src0 = f2 + (size_t)pch * HW2 + (size_t)(ylo + prow) * W2 + xs + ppc * G;
   PT buf[kIns];
   auto issue = [&](int u) __attribute__((always_inline)) {
     if (pv) {
-      const __half* su = src0 + (size_t)u * kNcChunk * HW2;
+      const T* su = src0 + (size_t)u * KC * HW2;
 #pragma unroll
-      for (int i = 0; i < kIns; i++) buf[i] = ldg<PT>(su + (size_t)(kCh * i) * HW2);
+      for (int i = 0; i < kIns; i++) buf[i] = ldg<PT>(su + (size_t)(CH * i) * HW2);
     }
   };
-  char* wb = wlds + (pch * P + prow * Wp + ppc * G) * 2;  // the lane's piece in channel row 0
+  // the lane's piece in channel row 0 of the image
+  char* wb = wlds + (size_t)(pch * P + prow * Wp + ppc * G) * sizeof(T);
   auto stage = [&]() __attribute__((always_inline)) {
     if (pv) {
 #pragma unroll
-      for (int i = 0; i < kIns; i++) *reinterpret_cast<PT*>(wb + kCh * i * P * 2) = buf[i];
+      for (int i = 0; i < kIns; i++)
+        *reinterpret_cast<PT*>(wb + (size_t)CH * i * P * sizeof(T)) = buf[i];
     }
   };
 
-  // gmap patch [C][np] (16-B units, C * np * 2 is a multiple of 16) -> LDS
-  // -> A fragments; its loads overlap chunk 0's
-  constexpr int kRA = (kNcC * kNcNpMax / 8 + kWave - 1) / kWave;
-  const int n16 = kNcC * np / 8;
+  // gmap patch [C][np] (16-B units, C * np * sizeof(T) is a multiple of 16) ->
+  // LDS -> A fragments; its loads overlap chunk 0's
+  constexpr int kPer16 = 16 / (int)sizeof(T);
+  constexpr int kRA = (kNcC * kNcNpMax / kPer16 + kWave - 1) / kWave;
+  const int n16 = kNcC * np / kPer16;
   u4 pa[kRA];
 #pragma unroll
-  for (int r = 0; r < kRA; r++) pa[r] = ldg<u4>(f1 + 8 * min(lane + kWave * r, n16 - 1));
+  for (int r = 0; r < kRA; r++) pa[r] = ldg<u4>(f1 + kPer16 * min(lane + kWave * r, n16 - 1));
   issue(0);
 #pragma unroll
   for (int r = 0; r < kRA; r++)
     if (lane + kWave * r < n16) reinterpret_cast<u4*>(wlds)[lane + kWave * r] = pa[r];
   wave_lds_sync();
   const int g4 = lane >> 4, am = lane & 15;
-  h8 A[kNcChunks];
-  {
+  const bool arow = am < np;
+  // A fragments: fp16 h8 per 32-channel chunk; fp32 one float per K step
+  h8 Ah[kHalf ? kChunks : 1];
+  float Af[kHalf ? 1 : kChunks * 4];
+  if constexpr (kHalf) {
     const _Float16* ph = reinterpret_cast<const _Float16*>(wlds);
-    const bool arow = am < np;
 #pragma unroll
-    for (int u = 0; u < kNcChunks; u++)
+    for (int u = 0; u < kChunks; u++)
 #pragma unroll
       for (int j = 0; j < 8; j++) {
-        const int c = kNcChunk * u + (j < 4 ? 4 * g4 + j : 16 + 4 * g4 + j - 4);
-        A[u][j] = arow ? ph[c * np + am] : (_Float16)0.0f;
+        const int c = KC * u + (j < 4 ? 4 * g4 + j : 16 + 4 * g4 + j - 4);
+        Ah[u][j] = arow ? ph[c * np + am] : (_Float16)0.0f;
+      }
+  } else {
+    const float* pf = reinterpret_cast<const float*>(wlds);
+#pragma unroll
+    for (int u = 0; u < kChunks; u++)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; s4++) {
+        const int c = KC * u + 4 * s4 + g4;
+        Af[4 * u + s4] = arow ? pf[c * np + am] : 0.0f;
       }
   }
   wave_lds_sync();  // patch read: the image may overwrite it
 
-  // transposed-read address of lane (g4, row q' = (lane >> 2) & 3, col 4 (lane & 3))
-  const char* ta = wlds + ((4 * g4 + ((lane >> 2) & 3)) * P + 4 * (lane & 3)) * 2;
-  const int ta1 = 16 * P * 2;  // the second read: channel rows 16 + 4 g4 + q'
+  // fp16: transposed-read address of lane (g4, row q' = (lane >> 2) & 3,
+  // col 4 (lane & 3)); fp32: B of K step s from channel row 4 s + g4, pixel am
+  const char* ta = kHalf ? wlds + ((4 * g4 + ((lane >> 2) & 3)) * P + 4 * (lane & 3)) * 2
+                         : wlds + (g4 * P + am) * 4;
+  const int ta1 = kHalf ? 16 * P * 2 : 4 * P * 4;  // fp16: rows 16 + 4 g4 + q'; fp32: next K step
   f4 acc[kNcMaxTiles];
 #pragma unroll
   for (int t = 0; t < kNcMaxTiles; t++) acc[t] = (f4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int u = 0; u < kNcChunks; u++) {
+  for (int u = 0; u < kChunks; u++) {
     stage();
     wave_lds_sync();
-    if (u + 1 < kNcChunks) issue(u + 1);
+    if (u + 1 < kChunks) issue(u + 1);
 #pragma unroll
     for (int t = 0; t < kNcMaxTiles; t++) {
       if (t < nt) {
-        const h4 b0 = tr_read(ta + 32 * t), b1 = tr_read(ta + ta1 + 32 * t);
-        const h8 bb = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[u], bb, acc[t], 0, 0, 0);
+        if constexpr (kHalf) {
+          const h4 b0 = tr_read(ta + 32 * t), b1 = tr_read(ta + ta1 + 32 * t);
+          const h8 bb = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah[u], bb, acc[t], 0, 0, 0);
+        } else {
+          float bv[4];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; s4++)
+            bv[s4] = *reinterpret_cast<const float*>(ta + s4 * ta1 + 64 * t);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; s4++)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(Af[4 * u + s4], bv[s4], acc[t], 0, 0, 0);
+        }
       }
     }
     wave_lds_sync();  // this chunk's reads before the next chunk's writes
@@ -196,13 +227,13 @@ __device__ __forceinline__ void nc_fast(const __half* __restrict__ fmap1,
   }
 }
 
-// One edge at one level; g = the level's widest piece (8 or 4 halves).
-__device__ __forceinline__ void nc_edge(const __half* __restrict__ fmap1,
-                                        const __half* __restrict__ f2lvl, int H2, int W2, int g,
-                                        float scale, bool use_scale,
+// One edge at one level; pbmax = the level's widest piece in bytes (16 or 8).
+template <typename T>
+__device__ __forceinline__ void nc_edge(const T* __restrict__ fmap1, const T* __restrict__ f2lvl,
+                                        int H2, int W2, int pbmax, float scale, bool use_scale,
                                         const float* __restrict__ coords, int b, int m, int ix,
                                         int jx, int M, int np, int N1, int N2, int R, char* wlds,
-                                        __half* __restrict__ out_t, float* __restrict__ out_f,
+                                        T* __restrict__ out_t, float* __restrict__ out_f,
                                         int out_stride, int out_off) {
   const int lane = threadIdx.x & (kWave - 1);
   const int D = 2 * R + 2, Dp = D - 1;
@@ -235,43 +266,48 @@ __device__ __forceinline__ void nc_edge(const __half* __restrict__ fmap1,
   int bw = xhi - xlo + 1, bh = yhi - ylo + 1;
   if (bw <= 0 || bh <= 0 || !idx_ok) bw = bh = 0;
   const int npx = bw * bh;
-  // image geometry: rows start at the G-aligned column xs <= xlo; 16-B pieces
-  // where the level allows them and the box fits one 2-channel instruction,
-  // else 8-B pieces (one channel per instruction), else the raw path
-  int xs = 0, npr = 0, Wp = 0, nt = 1, Gsel = 0;
-  auto fits = [&](int G, int lanes) {
+  // image geometry: rows start at the piece-aligned column xs <= xlo.  Load
+  // shape: 16-B pieces and 2 channels per instruction when the box fits 32
+  // lanes, else 16-B pieces and 1 channel, else 8-B pieces, else the raw path
+  int xs = 0, npr = 0, Wp = 0, nt = 1, mode = 0;
+  auto fits = [&](int pbytes, int lanes) {
+    const int G = pbytes / (int)sizeof(T);
     xs = xlo & ~(G - 1);
     npr = (xhi - xs) / G + 1;  // pieces per box row
     Wp = npr * G;
     nt = ((bh * Wp + 15) >> 4) | 1;  // odd tile count (bank-conflict-free reads)
     return nt <= kNcMaxTiles && bh * npr <= lanes;
   };
+  // (fp16 skips mode 2: 32 channels x 16 B per lane would be 128 VGPRs of loads)
+  constexpr bool kHalf = std::is_same<T, __half>::value;
   if (npx > 0) {
-    if (g == 8 && fits(8, kWave / 2)) Gsel = 8;
-    else if (fits(4, kWave)) Gsel = 4;
+    if (pbmax == 16 && fits(16, kWave / 2)) mode = 1;
+    else if (!kHalf && pbmax == 16 && fits(16, kWave)) mode = 2;
+    else if (fits(8, kWave)) mode = 3;
   }
-  const bool fast = Gsel != 0;
+  const bool fast = mode != 0;
   const int P = nt * 16;
   const int xoff = xlo - xs;
   const size_t HW2 = (size_t)H2 * W2;
 
-  if (Gsel == 8) {
-    nc_fast<8>(fmap1, f2lvl, H2, W2, b, ix, jx, np, N1, N2, ylo, bh, xs, npr, Wp, nt, wlds);
-  } else if (Gsel == 4) {
-    nc_fast<4>(fmap1, f2lvl, H2, W2, b, ix, jx, np, N1, N2, ylo, bh, xs, npr, Wp, nt, wlds);
+  if (mode == 1) {
+    nc_fast<T, 16, 2>(fmap1, f2lvl, H2, W2, b, ix, jx, np, N1, N2, ylo, bh, xs, npr, Wp, nt, wlds);
+  } else if (!kHalf && mode == 2) {
+    nc_fast<T, 16, 1>(fmap1, f2lvl, H2, W2, b, ix, jx, np, N1, N2, ylo, bh, xs, npr, Wp, nt, wlds);
+  } else if (mode == 3) {
+    nc_fast<T, 8, 1>(fmap1, f2lvl, H2, W2, b, ix, jx, np, N1, N2, ylo, bh, xs, npr, Wp, nt, wlds);
   } else if (npx > 0) {
     // ---- rare: windows too spread for the image; raw[k][yy][xx] directly ----
-    const __half* f2 = f2lvl + ((size_t)b * N2 + jx) * kNcC * HW2;
-    const __half* f1 = fmap1 + ((size_t)b * N1 + ix) * kNcC * np;
+    const T* f2 = f2lvl + ((size_t)b * N2 + jx) * kNcC * HW2;
+    const T* f1 = fmap1 + ((size_t)b * N1 + ix) * kNcC * np;
     const int nraw = np * D * D;
     for (int e = lane; e < nraw; e += kWave) {
       const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
       const int i1 = geo->y0[k] + yy - R, j1 = geo->x0[k] + xx - R;
       float s = 0.f;
       if (i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
-        const __half* p2 = f2 + (size_t)i1 * W2 + j1;
-        for (int c = 0; c < kNcC; c++)
-          s += __half2float(f1[c * np + k]) * __half2float(p2[(size_t)c * HW2]);
+        const T* p2 = f2 + (size_t)i1 * W2 + j1;
+        for (int c = 0; c < kNcC; c++) s += to_acc(f1[c * np + k]) * to_acc(p2[(size_t)c * HW2]);
       }
       Gs[e] = s;
     }
@@ -307,7 +343,7 @@ __device__ __forceinline__ void nc_edge(const __half* __restrict__ fmap1,
     v = v + ((1.f - dx) * dy) * r10;
     v = v + (dx * dy) * r11;
     if (out_t)
-      out_t[ebase + o] = __float2half(v);
+      out_t[ebase + o] = from_acc<T>(v);
     else
       out_f[(ebase + o) * out_stride + out_off] = v;
   }
@@ -412,11 +448,12 @@ __device__ __forceinline__ void nc_order(const int64_t* __restrict__ jj, int M, 
   __syncthreads();
 }
 
+template <typename T>
 __global__ void __launch_bounds__(kNcWaves* kWave, 2)  // 2 workgroups (8 waves) per CU
-    corr_nchw_kernel(const __half* __restrict__ fmap1, NcLevels lv, int use_scale,
+    corr_nchw_kernel(const T* __restrict__ fmap1, NcLevels lv, int use_scale,
                      const float* __restrict__ coords, const int64_t* __restrict__ ii,
                      const int64_t* __restrict__ jj, int B, int M, int np, int N1, int N2, int R,
-                     int L, int ordered, __half* __restrict__ out_t, float* __restrict__ out_f) {
+                     int L, int ordered, T* __restrict__ out_t, float* __restrict__ out_f) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wid = wave_uniform(threadIdx.x / kWave);
   char* wlds = smem + wid * kNcWaveBytes;
@@ -436,47 +473,22 @@ __global__ void __launch_bounds__(kNcWaves* kWave, 2)  // 2 workgroups (8 waves)
   const int l = blockIdx.y;
   const int b = unit / M, m = unit % M;
   const int ix = wave_uniform((int)ii[m]), jx = wave_uniform((int)jj[m]);
-  const __half* f2 = nc_sel(l, lv.f2[0], lv.f2[1], lv.f2[2], lv.f2[3]);
+  const T* f2 = reinterpret_cast<const T*>(nc_sel(l, lv.f2[0], lv.f2[1], lv.f2[2], lv.f2[3]));
   const int H2 = nc_sel(l, lv.H2[0], lv.H2[1], lv.H2[2], lv.H2[3]);
   const int W2 = nc_sel(l, lv.W2[0], lv.W2[1], lv.W2[2], lv.W2[3]);
-  const int g = nc_sel(l, lv.g[0], lv.g[1], lv.g[2], lv.g[3]);
+  const int pb = nc_sel(l, lv.pb[0], lv.pb[1], lv.pb[2], lv.pb[3]);
   const float s = nc_sel(l, lv.scale[0], lv.scale[1], lv.scale[2], lv.scale[3]);
-  nc_edge(fmap1, f2, H2, W2, g, s, use_scale != 0, coords, b, m, ix, jx, M, np, N1, N2, R, wlds,
-          out_t, out_f, L, l);
+  nc_edge<T>(fmap1, f2, H2, W2, pb, s, use_scale != 0, coords, b, m, ix, jx, M, np, N1, N2, R,
+             wlds, out_t, out_f, L, l);
 }
 
-}  // namespace
-
-// The matrix-core NCHW fp16 forward, or DPVO_ERR_UNSUPPORTED when the call is
-// outside its shape (then the caller runs corr.hip's VALU kernel): fp16, C =
-// 128, p*p <= 16, L <= 4, every level W2 % 4 == 0 with a piece-aligned base.
-// out_t: [B, M, Dp, Dp, p, p] fp16 (L = 1); else out_f [.., L] float32.
-int corr_nchw_mma(const void* fmap1, const void* const* fmap2, const int* H2, const int* W2,
-                  const float* scale, int L, bool use_scale, const float* coords,
-                  const int64_t* ii, const int64_t* jj, int B, int M, int C, int np, int N1,
-                  int N2, int R, int dtype, void* out_t, float* out_f, hipStream_t s) {
-  if (dtype != DPVO_F16 || C != kNcC || np < 1 || np > kNcNpMax || L < 1 || L > kNcMaxL ||
-      R < 0 || R > 7)
-    return DPVO_ERR_UNSUPPORTED;
-  if (out_t && L != 1) return DPVO_ERR_INVALID;
-  if (reinterpret_cast<uintptr_t>(fmap1) % 16) return DPVO_ERR_UNSUPPORTED;
-  NcLevels lv = {};
-  for (int l = 0; l < L; l++) {
-    const uintptr_t p = reinterpret_cast<uintptr_t>(fmap2[l]);
-    int g = 0;
-    if (W2[l] % 8 == 0 && p % 16 == 0) g = 8;
-    else if (W2[l] % 4 == 0 && p % 8 == 0) g = 4;
-    if (!g || H2[l] <= 0) return DPVO_ERR_UNSUPPORTED;
-    lv.f2[l] = reinterpret_cast<const __half*>(fmap2[l]);
-    lv.H2[l] = H2[l];
-    lv.W2[l] = W2[l];
-    lv.g[l] = g;
-    lv.scale[l] = scale ? scale[l] : 1.0f;
-  }
-  if ((long long)B * M == 0) return DPVO_OK;
+template <typename T>
+int nc_launch(const void* fmap1, const NcLevels& lv, bool use_scale, const float* coords,
+              const int64_t* ii, const int64_t* jj, int B, int M, int np, int N1, int N2, int R,
+              int L, int ordered, void* out_t, float* out_f, hipStream_t s) {
   static bool attr = false;  // 4 x 17.7 KB per workgroup (+ the order's 4 edge ids): above 64 KB
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)corr_nchw_kernel,
+    if (hipFuncSetAttribute((const void*)corr_nchw_kernel<T>,
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             kNcWaves * kNcWaveBytes + 16) != hipSuccess) {
       (void)hipGetLastError();  // not sticky: report it here, not at a later launch
@@ -484,25 +496,63 @@ int corr_nchw_mma(const void* fmap1, const void* const* fmap2, const int* H2, co
     }
     attr = true;
   }
+  unsigned gx = (unsigned)(((long long)B * M + kNcWaves - 1) / kNcWaves);
+  if (ordered) gx = 8u * ((gx + 7u) / 8u);
+  const dim3 grid(gx, L), block(kNcWaves * kWave);
+  hipLaunchKernelGGL(corr_nchw_kernel<T>, grid, block, (size_t)kNcWaves * kNcWaveBytes + 16, s,
+                     (const T*)fmap1, lv, use_scale ? 1 : 0, coords, ii, jj, B, M, np, N1, N2, R,
+                     L, ordered, (T*)out_t, out_f);
+  return launch_status();
+}
+
+}  // namespace
+
+// The matrix-core NCHW forward, or DPVO_ERR_UNSUPPORTED when the call is
+// outside its shape (then the caller runs corr.hip's VALU kernel): fp16 or
+// fp32, C = 128, p*p <= 16, L <= 4, every level with 8-B pieces at least
+// (W2 and the base aligned to 8 B).  out_t: [B, M, Dp, Dp, p, p] in the fmap
+// dtype (L = 1); else out_f [.., L] float32.
+int corr_nchw_mma(const void* fmap1, const void* const* fmap2, const int* H2, const int* W2,
+                  const float* scale, int L, bool use_scale, const float* coords,
+                  const int64_t* ii, const int64_t* jj, int B, int M, int C, int np, int N1,
+                  int N2, int R, int dtype, void* out_t, float* out_f, hipStream_t s) {
+  if ((dtype != DPVO_F16 && dtype != DPVO_F32) || C != kNcC || np < 1 || np > kNcNpMax ||
+      L < 1 || L > kNcMaxL || R < 0 || R > 7)
+    return DPVO_ERR_UNSUPPORTED;
+  if (out_t && L != 1) return DPVO_ERR_INVALID;
+  if (reinterpret_cast<uintptr_t>(fmap1) % 16) return DPVO_ERR_UNSUPPORTED;
+  const int es = dtype == DPVO_F16 ? 2 : 4;
+  NcLevels lv = {};
+  for (int l = 0; l < L; l++) {
+    const uintptr_t p = reinterpret_cast<uintptr_t>(fmap2[l]);
+    int pb = 0;  // widest piece whose alignment every row start keeps
+    if ((W2[l] * es) % 16 == 0 && p % 16 == 0) pb = 16;
+    else if ((W2[l] * es) % 8 == 0 && p % 8 == 0) pb = 8;
+    if (!pb || H2[l] <= 0) return DPVO_ERR_UNSUPPORTED;
+    lv.f2[l] = fmap2[l];
+    lv.H2[l] = H2[l];
+    lv.W2[l] = W2[l];
+    lv.pb[l] = pb;
+    lv.scale[l] = scale ? scale[l] : 1.0f;
+  }
+  if ((long long)B * M == 0) return DPVO_OK;
   // XCD-aware order for a single batch of a DPVO-sized graph, when some level's
   // ring is larger than the L2s together (8 x 4 MB): the order's prologue costs
   // ~6 us per workgroup and pays only where lines are re-fetched from the
-  // Infinity Cache / HBM (cfg2 level 1, 177 MB: 51 -> 31 us; level 4, 11 MB:
-  // 21 -> 23 us)
+  // Infinity Cache / HBM (cfg2 fp16 level 1, 177 MB: 51 -> 31 us; level 4,
+  // 11 MB: 21 -> 23 us)
   size_t ring = 0;
   for (int l = 0; l < L; l++) {
-    const size_t r = (size_t)N2 * kNcC * H2[l] * W2[l] * 2;
+    const size_t r = (size_t)N2 * kNcC * H2[l] * W2[l] * es;
     ring = r > ring ? r : ring;
   }
   const int ordered = B == 1 && M <= kOrdMaxE && N2 >= 1 && N2 <= kOrdMaxN2 &&
                       ring > ((size_t)32 << 20);
-  unsigned gx = (unsigned)(((long long)B * M + kNcWaves - 1) / kNcWaves);
-  if (ordered) gx = 8u * ((gx + 7u) / 8u);
-  const dim3 grid(gx, L), block(kNcWaves * kWave);
-  hipLaunchKernelGGL(corr_nchw_kernel, grid, block, (size_t)kNcWaves * kNcWaveBytes + 16, s,
-                     (const __half*)fmap1, lv, use_scale ? 1 : 0, coords, ii, jj, B, M, np, N1,
-                     N2, R, L, ordered, (__half*)out_t, out_f);
-  return launch_status();
+  if (dtype == DPVO_F16)
+    return nc_launch<__half>(fmap1, lv, use_scale, coords, ii, jj, B, M, np, N1, N2, R, L,
+                             ordered, out_t, out_f, s);
+  return nc_launch<float>(fmap1, lv, use_scale, coords, ii, jj, B, M, np, N1, N2, R, L, ordered,
+                          out_t, out_f, s);
 }
 
 }  // namespace dpvo

@@ -485,3 +485,43 @@ def test_nchw_fp16_cfg2_matches_channels_last(cc, gpu):
                               (coords / s).cpu().numpy()[:, sel], kk1.cpu().numpy()[sel],
                               jj1.cpu().numpy()[sel], 3)
         _close_f16(a64[:, sel], ref)
+
+
+# ---- NCHW fp32 levels: the same kernel with 16-channel images and
+# v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 sums): the fp32 bar
+@pytest.mark.parametrize("kw", [
+    dict(),                                   # W2 = 32: 16-B pieces, 2 channels / load
+    dict(W2=34, M=60),                        # W2 * 4 % 16 == 8: 8-B pieces
+    dict(W2=36, spread=1.0, M=120),           # wide boxes: 1 channel / load, raw-path edges
+    dict(R=1), dict(R=7), dict(p=2), dict(p=4), dict(Hp=2, Wp=3),
+    dict(far=0.5), dict(B=2, M=11), dict(H2=5, W2=8, M=21),
+    dict(M=300, H2=40, W2=48),
+])
+def test_nchw_fp32_forward_matches_oracle(cc, gpu, kw):
+    f1, f2, co, ii, jj, R = _case(31, **kw)
+    out, = cc.forward(_t(f1, gpu), _t(f2, gpu), _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R)
+    assert out.dtype == torch.float32
+    _close(out.cpu().numpy(), oracle.corr_fwd(f1, f2, co, ii, jj, R))
+
+
+def test_nchw_fp32_cfg2_matches_channels_last(cc, gpu):
+    """fp32 drop-in at full cfg2 size (36-frame ring, ordered path) against
+    the channels-last kernel on the same data and the oracle on a sample."""
+    from dpvo_amd import fastba, synthetic
+
+    G = synthetic.make_config("cfg2", seed=8)
+    D = G.to(gpu)
+    mem, levels = 36, (1, 4)
+    coords = fastba.reproject(D.poses, D.patches, D.intrinsics, D.ii, D.jj, D.kk)
+    pyr = synthetic.make_features(mem=mem, C=128, levels=levels, seed=4, device=gpu)
+    gmap = 0.25 * torch.randn(1, mem * G.M, 128, 3, 3, device=gpu)
+    kk1, jj1 = D.kk % (mem * G.M), D.jj % mem
+    sel = np.arange(0, G.E, 41)
+    for l, s in enumerate(levels):
+        a, = cc.forward(gmap, pyr[l], coords / s, kk1, jj1, 3)
+        b, = cc.forward(gmap, synthetic.channels_last(pyr[l]), coords / s, kk1, jj1, 3)
+        _close(a.cpu().numpy(), b.cpu().numpy(), 1e-5)
+        ref = oracle.corr_fwd(gmap.cpu().numpy(), pyr[l].cpu().numpy(),
+                              (coords / s).cpu().numpy()[:, sel], kk1.cpu().numpy()[sel],
+                              jj1.cpu().numpy()[sel], 3)
+        _close(a.cpu().numpy()[:, sel], ref)
