@@ -44,7 +44,8 @@ constexpr int kMaxFree = 20;  // pose-block masks are 32-bit; lower S blocks of 
 constexpr int kPerThread = kMaxSetupE / kSetupThreads;
 constexpr int kCtlBytes = 512;
 constexpr int kSetupLds = 160 * 1024;
-constexpr int kMarks = 2176;  // [0, 128) phases; window kernel per workgroup: [128 + 256 it + g] assembled, [640 + 256 it + g] all partials seen, [1152 + g] setup, [1408 + g] it 0 pre-reduction; dense kernel: [1664 + g] it 0 linearised, [1920 + g] own edges | patches << 16
+constexpr int kMarks = 2176;  // [0, 128) phases; window kernel per workgroup: [128 + 256 it + g] assembled, [640 + 256 it + g] all partials seen, [1152 + g] setup, [1408 + g] it 0 pre-reduction; fused reproject + plan + insert launch: [1664 + 2b] / [1665 + 2b] start / end of workgroup b
+constexpr int kLaunchMarks = 1664;
 constexpr int kNoPose = 31;
 constexpr int kEC = 16;  // doubles per position record of E terms
 
@@ -1049,7 +1050,7 @@ int ba_window_reproject_plan_insert(const float* poses, const float* patches,
                                     int num_patches, int N2, float* coords, int* order, int t0,
                                     int t1, char* scratch, int* status, const void* src,
                                     void* const* dst, const int* scale, int L, int C, int H, int W,
-                                    int half, void* stream);
+                                    int half, int64_t* marks, void* stream);
 int ba_window_run(float* poses, float* patches, const float* intrinsics, const float* target,
                   const float* weight, const float* lmbda, const int64_t* ii, const int64_t* jj,
                   const int64_t* kk, int E, int P, int num_poses, int num_patches, int t0, int t1,
@@ -1489,7 +1490,8 @@ DPVO_EXPORT int dpvo_reproject_ordered_plan_insert(
   return ba_window_reproject_plan_insert(poses, patches, intrinsics, ii, jj, kk, E, P, num_poses,
                                          num_patches, N2, coords, (int*)order, t0, t1,
                                          (char*)workspace + base_bytes, w.meta + 1, src, dst,
-                                         scale, L, C, H, W, dtype == DPVO_F16 ? 1 : 0, stream);
+                                         scale, L, C, H, W, dtype == DPVO_F16 ? 1 : 0,
+                                         g_ba_marks ? w.tmark + kLaunchMarks : nullptr, stream);
 }
 
 DPVO_EXPORT int dpvo_reproject_ordered_plan_dev(const float* poses, const float* patches,

@@ -77,7 +77,7 @@ constexpr int kStChol = 1, kStClamp = 2, kStTimeout = 16, kStCap = 32;
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // plan meta (ints): [0] nuniq, [1] fmin, [2] status, [3] shards that wrote
-// block-work partials; [16, 28) int64 phase stamps; [kMetaWork + lblk(a, b)
+// block-work partials; [16, 34) int64 phase stamps + 2 shader clocks; [kMetaWork + lblk(a, b)
 // * kPlanShardMax + s] edges of the patches whose free poses hold a and b, from
 // shard s (ba_window_kernel gives each lower block workgroups in proportion;
 // a block's 16 shard counts are one 64-B run: four 16-B loads)
@@ -181,11 +181,12 @@ constexpr int kPlanPer = kWMaxE / kPT;  // edges per plan thread: e = tid + r * 
 // before its first use (one global round trip per round, and only the rounds
 // that hold edges); indices are clamped instead of guarded (a guarded load is
 // a branch with its own wait).  Ends with a barrier.
+template <int kPer = kPlanPer>
 __device__ __forceinline__ void plan_edges_pass(const int64_t* __restrict__ ii,
                                                 const int64_t* __restrict__ jj,
                                                 const int64_t* __restrict__ kk, int E,
                                                 int num_patches, int num_poses, int t0, int N,
-                                                int* ctl, unsigned short* code, int (&kv)[kPlanPer]) {
+                                                int* ctl, unsigned short* code, int (&kv)[kPer]) {
   const int tid = threadIdx.x, lane = tid & 63, T = kPT;
   const int kmaxc = num_patches - 1;
   if (tid == 0) {
@@ -195,14 +196,14 @@ __device__ __forceinline__ void plan_edges_pass(const int64_t* __restrict__ ii,
     ctl[3] = 0;           // status
   }
   __syncthreads();
-  constexpr int kPlanRound = 5;
-  static_assert(kPlanPer % kPlanRound == 0, "load rounds");
+  constexpr int kPlanRound = kPer % 5 == 0 ? 5 : kPer;
+  static_assert(kPer % kPlanRound == 0, "load rounds");
   int kmin = 0x7fffffff, kmax = -1, fmin = 0x7fffffff, bad = 0;
 #pragma unroll
-  for (int r = 0; r < kPlanPer; r++) kv[r] = 0;
+  for (int r = 0; r < kPer; r++) kv[r] = 0;
   if (E > 0) {
 #pragma unroll
-    for (int r0 = 0; r0 < kPlanPer; r0 += kPlanRound) {
+    for (int r0 = 0; r0 < kPer; r0 += kPlanRound) {
       if (r0 * T >= E) break;  // block-uniform: only the rounds that hold edges (one at cfg2)
       int64_t vk[kPlanRound], vi[kPlanRound], vj[kPlanRound];
 #pragma unroll
@@ -514,21 +515,26 @@ __device__ __forceinline__ void plan_block(const int64_t* __restrict__ ii,
 __host__ __device__ constexpr int plan_shards(int E) {
   return E <= 512 ? 1 : ((E + 511) / 512 < kPlanShardMax ? (E + 511) / 512 : kPlanShardMax);
 }
-__device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
+template <int kPer>
+__device__ __forceinline__ void plan_sharded_k(const int64_t* __restrict__ ii,
                                              const int64_t* __restrict__ jj,
-                                             const int64_t* __restrict__ kk, int E, int num_patches,
-                                             int num_poses, int t0, int N, const Plan& plan,
-                                             char* lds, int cap, size_t lds_bytes, int s, int S) {
+                                               const int64_t* __restrict__ kk, int E, int num_patches,
+                                               int num_poses, int t0, int N, const Plan& plan,
+                                               char* lds, int cap, size_t lds_bytes, int s, int S) {
   if (S <= 1) {
     if (s == 0) plan_block(ii, jj, kk, E, num_patches, num_poses, t0, N, plan, lds, cap);
     return;
   }
   if (plan.t0d) t0 = *plan.t0d;
-  // phase stamps of shard 0 (100 MHz wall clock, 8 stores per launch):
-  // meta + 16 as int64 [6] (scripts/plan_phases.py)
+  // phase stamps of shard 0 (100 MHz wall clock, 7 stores per launch):
+  // meta + 16 as int64 [7], then the shader clock at stamps 0 and 6
+  // (scripts/plan_phases.py)
   auto stamp = [&](int q) {
-    if (s == 0 && threadIdx.x == 0)
+    if (s == 0 && threadIdx.x == 0) {
       reinterpret_cast<int64_t*>(plan.meta + 16)[q] = (int64_t)wall_clock64();
+      // shader clock at the first and last stamp: the effective frequency
+      if (q == 0 || q == 6) reinterpret_cast<int64_t*>(plan.meta + 16)[7 + (q == 6)] = (int64_t)clock64();
+    }
   };
   stamp(0);
   //   [ctl 256 B | code u16[cap] | spos u16[cap] | hf int[R] | pm u32[nl]]
@@ -538,8 +544,8 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
   unsigned short* code = (unsigned short*)(lds + 256);
   unsigned short* spos = code + cap;
   int* hf = reinterpret_cast<int*>(spos + cap);  // histogram of kk - kmin over the FULL range
-  int kv[kPlanPer];
-  plan_edges_pass(ii, jj, kk, E, num_patches, num_poses, t0, N, ctl, code, kv);
+  int kv[kPer];
+  plan_edges_pass<kPer>(ii, jj, kk, E, num_patches, num_poses, t0, N, ctl, code, kv);
   stamp(1);
   const int kmin = ctl[0], R = ctl[1] - kmin + 1;
   const int nlmax = (R + S - 1) / S;
@@ -570,7 +576,7 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
   // bitmap word took 32 patches' worth of atomics)
   int nb = 0;
 #pragma unroll
-  for (int r = 0; r < kPlanPer; r++) {
+  for (int r = 0; r < kPer; r++) {
     const int e = tid + r * T;
     if (e >= E) continue;
     const int v = kv[r] - kmin;
@@ -600,7 +606,7 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
   stamp(3);
   const int below = ctl[4], ubelow = ctl[5], nuniq = ctl[6];
 #pragma unroll
-  for (int r = 0; r < kPlanPer; r++) {
+  for (int r = 0; r < kPer; r++) {
     const int e = tid + r * T;
     const int v = kv[r] - kmin - lo;
     if (e >= E || v < 0 || v >= nl) continue;
@@ -618,8 +624,9 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
     c = (hv >> 14) - (v == 0 ? 0 : (hist[v - 1] >> 14));
     m = pm[hv & 0x3fff];
   }, wl);
+  stamp(5);
 #pragma unroll
-  for (int r = 0; r < kPlanPer; r++) {
+  for (int r = 0; r < kPer; r++) {
     const int e = tid + r * T;
     const int v = kv[r] - kmin - lo;
     if (e >= E || v < 0 || v >= nl) continue;
@@ -645,7 +652,23 @@ __device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
     if (ctl[3] && plan.sink) atomicOr(plan.sink, ctl[3]);
     *plan.status = 0;
   }
-  stamp(5);
+  stamp(6);
+}
+
+// The executed code of the plan is what a cold instruction cache pays for
+// (the launch follows A-CORR and the BA window, which evict it): graphs of up
+// to 4 edges per thread (E <= 2048, cfg2) run a copy unrolled 4 deep instead
+// of kPlanPer = 20.
+__device__ __forceinline__ void plan_sharded(const int64_t* __restrict__ ii,
+                                             const int64_t* __restrict__ jj,
+                                             const int64_t* __restrict__ kk, int E, int num_patches,
+                                             int num_poses, int t0, int N, const Plan& plan,
+                                             char* lds, int cap, size_t lds_bytes, int s, int S) {
+  if (E <= 4 * kPT)
+    plan_sharded_k<4>(ii, jj, kk, E, num_patches, num_poses, t0, N, plan, lds, cap, lds_bytes, s, S);
+  else
+    plan_sharded_k<kPlanPer>(ii, jj, kk, E, num_patches, num_poses, t0, N, plan, lds, cap,
+                             lds_bytes, s, S);
 }
 
 __global__ void __launch_bounds__(kPT) ba_plan_kernel(const int64_t* __restrict__ ii,
@@ -674,6 +697,7 @@ struct RArgs {
   float* coords;
   int* order;
   int nps;  // plan shards: workgroups [0, nps) plan, nps the edge order, then the reprojection
+  int64_t* marks;  // instrumentation (dpvo_ba_set_marks): [2b] / [2b + 1] start / end of workgroup b < 256
 };
 
 __global__ void __launch_bounds__(kPT) reproject_plan_kernel(RArgs R, Plan plan) {
@@ -707,10 +731,12 @@ struct InsArgs {
 };
 
 template <typename T>
-__global__ void __launch_bounds__(kPT) reproject_plan_insert_kernel(RArgs R, Plan plan, InsArgs I,
-                                                                    int nrep) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
+__device__ __forceinline__ void reproject_plan_insert_body(const RArgs& R, const Plan& plan,
+                                                           const InsArgs& I, int nrep, char* lds) {
   const int b = blockIdx.x, b0 = R.nps + 1;  // first reprojection workgroup
+  // the plan shards and the edge order are the launch's long chains; the
+  // insertion tiles share their CUs: their waves issue first
+  if (b <= R.nps) __builtin_amdgcn_s_setprio(3);
   if (b < R.nps) {
     plan_sharded(R.ii, R.jj, R.kk, R.E, R.num_patches, R.num_poses, R.t0, R.N, plan, lds,
                  plan_cap(R.E), plan_lds_bytes(plan_cap(R.E)), b, R.nps);
@@ -735,6 +761,19 @@ __global__ void __launch_bounds__(kPT) reproject_plan_insert_kernel(RArgs R, Pla
   float* tile = reinterpret_cast<float*>(lds) + half * kInsTC * kInsCS;
   ins_tile<T>(static_cast<const T*>(I.src), I.lv, I.L, I.C, I.H, I.W, tt % I.gx,
               (tt / I.gx) % I.gy, tt / (I.gx * I.gy), threadIdx.x & 255, act, tile);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kPT) reproject_plan_insert_kernel(RArgs R, Plan plan, InsArgs I,
+                                                                    int nrep) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const bool mk = R.marks && blockIdx.x < 256;
+  if (mk && threadIdx.x == 0) R.marks[2 * blockIdx.x] = (int64_t)wall_clock64();
+  reproject_plan_insert_body<T>(R, plan, I, nrep, lds);
+  if (mk) {
+    __syncthreads();
+    if (threadIdx.x == 0) R.marks[2 * blockIdx.x + 1] = (int64_t)wall_clock64();
+  }
 }
 
 // ===========================================================================
@@ -2099,6 +2138,7 @@ int ba_window_reproject_plan(const float* poses, const float* patches, const flo
   Plan plan = plan_view(scratch, E, status);
   plan.t0d = t0d;
   RArgs r;
+  r.marks = nullptr;
   r.poses = poses;
   r.patches = patches;
   r.intrinsics = intrinsics;
@@ -2129,11 +2169,12 @@ int ba_window_reproject_plan_insert(const float* poses, const float* patches,
                                     int num_patches, int N2, float* coords, int* order, int t0,
                                     int t1, char* scratch, int* status, const void* src,
                                     void* const* dst, const int* scale, int L, int C, int H, int W,
-                                    int half, void* stream) {
+                                    int half, int64_t* marks, void* stream) {
   set_attrs();
   Plan plan = plan_view(scratch, E, status);
   plan.t0d = nullptr;
   RArgs r;
+  r.marks = marks;
   r.poses = poses;
   r.patches = patches;
   r.intrinsics = intrinsics;

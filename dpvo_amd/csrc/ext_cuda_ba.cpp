@@ -286,6 +286,15 @@ torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
   return torch::cat({out, wg});
 }
 
+// The marks a workspace holds (after launches made with set_marks(true)).
+torch::Tensor ba_workspace_marks(torch::Tensor ws, int64_t E, int t0, int t1) {
+  auto out = torch::zeros({2176}, ws.options().dtype(torch::kInt64));
+  check_status(dpvo_ba_phase_marks(ws.data_ptr(), (int)E, t0, t1, out.data_ptr<int64_t>(),
+                                   current_stream()),
+               "cuda_ba.workspace_marks");
+  return out;
+}
+
 // Same call; returns the pose step dX [N, 6] (fp64) of the last iteration
 // (ba_cuda.cu:561-562) -- the parity tests' view of the solve.
 torch::Tensor ba_forward_dx(torch::Tensor poses, torch::Tensor patches, torch::Tensor intrinsics,
@@ -1053,6 +1062,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gba_solve_update", &gba_solve_update, "large-graph BA: solve + retraction");
   m.def("gba_info", &gba_info, "status, nuniq, nitems, nblk, nI, nB, g, nsb (device int32[8])");
   m.def("forward_marks", &ba_forward_marks, "forward + per-phase wall-clock marks");
+  m.def("set_marks", [](bool on) { check_status(dpvo_ba_set_marks(on ? 1 : 0), "set_marks"); },
+        "stamp wall-clock marks into the BA workspace (instrumentation)");
+  m.def("workspace_marks", &ba_workspace_marks,
+        "the 2176 marks of a workspace ([1664 + 2b] / [1665 + 2b]: fused launch workgroup b)");
   m.def("forward_dx", &ba_forward_dx, "forward; returns the last iteration's dX [N, 6] (fp64)");
   m.def("last_dx", &ba_last_dx, "dX [N, 6] of the last iteration of a planned forward on ws");
   m.def("reproject_ordered_plan", &ba_reproject_ordered_plan,

@@ -17,13 +17,13 @@ import torch  # noqa: E402
 from dpvo_amd import fastba, synthetic  # noqa: E402
 from dpvo_amd._native import load_extension  # noqa: E402
 
-NAMES = ["edge pass", "presence + histogram", "local scan", "scatter", "rank + stores"]
+NAMES = ["edge pass", "presence + histogram", "local scan", "scatter", "block work", "rank + stores"]
 
 
 def stamps(cb, ws, E, t0, t1):
     off = cb.plan_offsets(E, t0, t1)
     b = ws.cpu().numpy().tobytes()
-    return np.frombuffer(b[off[4] + 64:off[4] + 64 + 48], np.int64)
+    return np.frombuffer(b[off[4] + 64:off[4] + 64 + 72], np.int64)
 
 
 def main():
@@ -55,10 +55,13 @@ def main():
                 torch.cuda.synchronize()
                 if rep >= 10:
                     st = stamps(cb, ws, G.E, t0, t1)
-                    rows.append(np.diff(st) * 0.01)
+                    ph = np.diff(st[:7]) * 0.01
+                    # shader-clock cycles / wall us over the plan = clock in MHz
+                    rows.append(np.append(ph, (st[8] - st[7]) / max(ph.sum(), 1e-3)))
             med = np.median(np.array(rows), axis=0)
             print(f"{name} E={G.E} {k}: " + ", ".join(f"{n} {v:.2f}" for n, v in zip(NAMES, med))
-                  + f" us; total {med.sum():.2f} us", flush=True)
+                  + f" us; total {med[:-1].sum():.2f} us; shader clock {med[-1]:.0f} MHz",
+                  flush=True)
 
 
 if __name__ == "__main__":
