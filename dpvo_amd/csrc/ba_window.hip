@@ -823,7 +823,8 @@ struct WL {  // LDS layout of one workgroup
   }
 };
 
-enum { cNrel = 0, cNrp = 1, cFmin = 2, cFail = 3, cTimeout = 4, cCap = 5, cFailAny = 6, cScan = 16 };
+enum { cNrel = 0, cNrp = 1, cFmin = 2, cFail = 3, cTimeout = 4, cCap = 5, cFailAny = 6, cLMulti = 7,
+       cScan = 16 };
 
 // E^T dX over relevant edges [q0, q1) (ba_cuda.cu:563), in order (patch_etdx:
 // all edges of relevant patch ri).  The E
@@ -1233,6 +1234,15 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   // ordered before its readers by the setup's barriers.
   int* bstart = reinterpret_cast<int*>(lds + off);  // [NB + 1]
   off = al16(off + sizeof(int) * (kWMaxNB + 1));
+  // gather destination of each slot: 36 lblk(a, b) (its block's place in S)
+  // for a lower block with one share, whose partial IS the block; -1 for the
+  // slots whose block sums several shares (diagonal blocks, split lower blocks)
+  int* sdst = reinterpret_cast<int*>(lds + off);  // [G]
+  off = al16(off + sizeof(int) * kWMaxG);
+  // the split lower blocks (o | lblk << 16), ctl[cLMulti] of them
+  int* mlist = reinterpret_cast<int*>(lds + off);  // [NB - N]
+  off = al16(off + sizeof(int) * kWMaxNB);
+  for (int sl = tid; sl < A.G; sl += kWT) sdst[sl] = -1;
   const int gd = N * A.Sd, nlow = NB - N;
   const int gx = A.G - gd - nlow;  // shares beyond Sd per diagonal and one per lower block
   int blk = 0, sub = 0, S = 1;
@@ -1328,6 +1338,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     ctl[cFailAny] = 0;
     ctl[cTimeout] = 0;
     ctl[cCap] = 0;
+    ctl[cLMulti] = 0;
   }
   int* cnt = (int*)(lds + off);  // [nuniq] scan input / prefix (kept until the records are built)
   auto relevant = [&](unsigned m, int u) {
@@ -1358,6 +1369,15 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   }
   mark(A, 40);
   __syncthreads();
+  for (int o = tid; o < NB - N; o += kWT) {  // bstart complete after the barrier above
+    const int s0 = bstart[N + o], s1 = bstart[N + o + 1];
+    int aa = 1;
+    while ((aa + 1) * aa / 2 <= o) aa++;  // lblk(aa, o - aa (aa - 1) / 2) = o + aa
+    if (s1 - s0 == 1)
+      sdst[s0] = 36 * (o + aa);
+    else if (s1 - s0 > 1)
+      mlist[atomicAdd(&ctl[cLMulti], 1)] = o | ((o + aa) << 16);  // any order: sums are per block
+  }
   const int tot = fscan(cnt, nuniq, scr);
   mark(A, 41);
   int nrel = tot >> 16, nrp = tot & 0xffff;
@@ -1616,13 +1636,8 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     double* red = reinterpret_cast<double*>(L.region);
     const unsigned long long gkey = (unsigned long long)(epoch * 64 + it + 1) ^ A.salt;
     const unsigned gtag = (unsigned)gkey;
-#if defined(BA_XCHG_FLAGS) || defined(BA_XCHG_FENCES)
-    v4u* const gbuf = nullptr;
-    v4u* const gslot = nullptr;
-#else
     v4u* const gbuf = A.gran + (size_t)(it & 1) * A.G * kGranPad;
     v4u* const gslot = gbuf + (size_t)g * kGranPad;
-#endif
     if (NB == 0) {
       assemble<0>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
     } else if (diag) {
@@ -1643,7 +1658,6 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     double* Sd = reinterpret_cast<double*>(L.region);
     double* yd = Sd + 36 * NB;
     double* pc = yd + 6 * N;  // [G][kPartPad] copy of the partials
-#if !defined(BA_XCHG_FLAGS) && !defined(BA_XCHG_FENCES)
     // the reduction scratch (red, seg) and pc share L.region: no thread may
     // write pc before the publishing threads have read their sums
     __syncthreads();
@@ -1655,6 +1669,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     {
       const int ndg = bstart[NNb];  // diagonal blocks' workgroups first: 27 granules, the others 36
       const int T = ndg * 27 + (A.G - ndg) * 36;
+      const int pcoff = (int)(pc - Sd);
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           gbuf, 0, (int)(16 * kGranPad * (size_t)A.G), kBufDword3);
       constexpr int kIn = 16;
@@ -1676,7 +1691,9 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
             k = u - 36 * (u / 36);
           }
           off[r] = 16 * (sl * kGranPad + k);
-          pos[r] = sl * kPartPad + k;
+          // its place: in S for a one-share lower block, else in the partials copy
+          const int sd = sdst[sl];
+          pos[r] = sd >= 0 ? sd + k : pcoff + sl * kPartPad + k;
           pend |= (t0_ + r * kWT < T) ? (1u << r) : 0u;
         }
         while (pend) {
@@ -1688,7 +1705,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
           for (int r = 0; r < kIn; r++) {
             const bool ok = ((pend >> r) & 1u) && v[r].w == gtag && v[r].z == gran_hash(v[r].x, v[r].y, gkey);
             if (ok) {
-              pc[pos[r]] = __longlong_as_double((long long)(((unsigned long long)v[r].y << 32) | v[r].x));
+              Sd[pos[r]] = __longlong_as_double((long long)(((unsigned long long)v[r].y << 32) | v[r].x));
               pend &= ~(1u << r);
             }
           }
@@ -1704,112 +1721,37 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     }
     mark(A, mb + 1);
     if (A.marks && tid == 0 && it < 2 && g < 256) A.marks[640 + 256 * it + g] = (int64_t)wall_clock64();
-#else
     __syncthreads();
-    // Hand-off without fences (MI355X_MICROARCH.md, inter-workgroup visibility:
-    // the first row of the sc1 hand-off table, one workgroup per CU, hipMalloc
-    // memory): the partial is stored sc1 by one wave that drains its stores
-    // before the barrier above (reduce_acc); one lane then stores the flag
-    // sc1; readers poll it sc1 and, after a workgroup barrier, load every byte
-    // of the partials with sc1 loads.  An agent release + acquire pair costs
-    // ~1.7 + 1.7 us per exchange on gfx950 (the guide's price list).
-#ifdef BA_XCHG_FENCES  // the fenced form (A/B timing)
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&A.flags[g], epoch * 64 + it + 1, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-#else
-    if (tid == 0)
-      __hip_atomic_store(&A.flags[g], epoch * 64 + it + 1, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-#endif
-    // ---- wait for every partial, gather S and y in a fixed order ----
-    if (tid < 64) {
-      bool ok = true;
-      for (int w = tid; w < A.G; w += 64) ok = wait_flag(&A.flags[w], epoch * 64 + it + 1) && ok;
-      if (!ok) ctl[cTimeout] = 1;
-#ifdef BA_XCHG_FENCES
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-    }
-    __syncthreads();
-    mark(A, mb + 1);
-    if (A.marks && tid == 0 && it < 2 && g < 256) A.marks[640 + 256 * it + g] = (int64_t)wall_clock64();
-#ifdef BA_XCHG_FENCES
+    mark(A, mb + 5);  // every thread's granules in LDS
     {
-      // 16-B plain loads (after the acquire above), kIn in flight per thread:
-      // one round for G <= 256
-      const int tot_p = kPartPad / 2 * A.G;
-      const double2* src = reinterpret_cast<const double2*>(pbuf);
-      double2* dst = reinterpret_cast<double2*>(pc);
-      constexpr int kIn = 24;
-      for (int t0_ = tid; t0_ < tot_p; t0_ += kIn * kWT) {
-        double2 v[kIn];
-#pragma unroll
-        for (int r = 0; r < kIn; r++) {
-          const int t = t0_ + r * kWT;
-          v[r] = (t < tot_p) ? src[t] : make_double2(0.0, 0.0);
-        }
-#pragma unroll
-        for (int r = 0; r < kIn; r++)
-          if (t0_ + r * kWT < tot_p) dst[t0_ + r * kWT] = v[r];
-      }
-    }
-#else
-    {
-      // the kPart / 2 used 16-B pairs of every slot as 16-B sc1 buffer loads
-      // (the builtin's cache-policy bit 4 is sc1 on gfx950; the compiler tracks
-      // them, so its own waits cover every use), kIn in flight per thread: one
-      // round for G <= 256
-      constexpr int kHalfPart = kPart / 2;
-      static_assert(kPart % 2 == 0 && kPartPad % 2 == 0, "16-B pairs");
-      const int tot_p = kHalfPart * A.G;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          pbuf, 0, (int)(sizeof(double) * kPartPad * A.G), kBufDword3);
-      constexpr int kIn = 12;
-      for (int t0_ = tid; t0_ < tot_p; t0_ += kIn * kWT) {
-        f64x2 v[kIn];
-#pragma unroll
-        for (int r = 0; r < kIn; r++) {
-          const int t = min(t0_ + r * kWT, tot_p - 1), sl = t / kHalfPart, k = t - sl * kHalfPart;
-          v[r] = __builtin_bit_cast(
-              f64x2, __builtin_amdgcn_raw_buffer_load_b128(
-                         rs, (int)(sizeof(double) * ((size_t)sl * kPartPad + 2 * k)), 0, kSc1));
-        }
-#pragma unroll
-        for (int r = 0; r < kIn; r++) {
-          const int t = t0_ + r * kWT, sl = t / kHalfPart, k = t - sl * kHalfPart;
-          if (t < tot_p) *reinterpret_cast<f64x2*>(pc + (size_t)sl * kPartPad + 2 * k) = v[r];
+      // The blocks that sum several shares, in share order: every diagonal
+      // block (21 stored entries mirrored to 36, and its 6 y entries) and the
+      // split lower blocks, if any; a one-share lower block is already in S.
+      // (One wave per SIMD: the cost here is instruction issue, so the work is
+      // only what needs summing -- summing all 36 NB + 6 N entries from the
+      // partials copy was 3.3 us per iteration.)
+      for (int t = tid; t < 42 * N; t += kWT) {
+        const int p = t / 42, e = t - 42 * p;
+        const int x = e / 6, z = e - 6 * x;  // e >= 36: y entry z (x == 6)
+        const int xx = max(x, z), zz = min(x, z);
+        const int idx = (x == 6) ? 21 + z : xx * (xx + 1) / 2 + zz;
+        const int s0 = bstart[p], s1 = bstart[p + 1];
+        double sv = 0.0;
+        for (int sb = s0; sb < s1; sb++) sv += pc[sb * kPartPad + idx];
+        if (x == 6) {
+          yd[6 * p + z] = sv;
+        } else {
+          if (x == z) sv += 1e-4 * sv + 1.0;  // S += I (1e-4 S + 1) (ba_cuda.cu:560)
+          Sd[36 * lblk(p, p) + e] = sv;
         }
       }
-    }
-#endif
-#endif
-    __syncthreads();
-    for (int t = tid; t < 36 * NB; t += kWT) {
-      const int blk = t / 36, k = t % 36;
-      const int ba_ = L.tri[blk] >> 8, bb_ = L.tri[blk] & 0xff;
-      double s = 0.0;
-      if (ba_ == bb_) {  // diagonal: 21 lower entries stored; mirror
-        const int x = k / 6, z = k % 6;
-        const int xx = x >= z ? x : z, zz = x >= z ? z : x;
-        const int li = xx * (xx + 1) / 2 + zz;
-        for (int sb = bstart[ba_]; sb < bstart[ba_ + 1]; sb++) s += pc[sb * kPartPad + li];
-        if (x == z) s += 1e-4 * s + 1.0;  // S += I (1e-4 S + 1) (ba_cuda.cu:560)
-      } else {
-        const int o = ba_ * (ba_ - 1) / 2 + bb_;
-        for (int sb = bstart[NNb + o]; sb < bstart[NNb + o + 1]; sb++) s += pc[sb * kPartPad + k];
+      for (int t = tid; t < 36 * ctl[cLMulti]; t += kWT) {
+        const int q = t / 36, k = t - 36 * q, ol = mlist[q], o = ol & 0xffff;
+        const int s0 = bstart[N + o], s1 = bstart[N + o + 1];
+        double sv = 0.0;
+        for (int sb = s0; sb < s1; sb++) sv += pc[sb * kPartPad + k];
+        Sd[36 * (ol >> 16) + k] = sv;
       }
-      Sd[t] = s;
-    }
-    for (int t = tid; t < 6 * N; t += kWT) {
-      const int i = t / 6, x = t % 6;
-      double s = 0.0;
-      for (int sb = bstart[i]; sb < bstart[i + 1]; sb++) s += pc[sb * kPartPad + 21 + x];
-      yd[t] = s;
     }
     __syncthreads();
     mark(A, mb + 2);

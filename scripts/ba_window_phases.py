@@ -55,6 +55,8 @@ for rep in range(40):
         d[f"it{it}: reduce + publish"] = (m[mb] - m[mb + 4]) * 0.01
         d[f"it{it}: wait partials"] = (m[mb + 1] - m[mb]) * 0.01
         d[f"it{it}: gather"] = (m[mb + 2] - m[mb + 1]) * 0.01
+        d[f"it{it}:   last granules"] = (m[mb + 5] - m[mb + 1]) * 0.01
+        d[f"it{it}:   sum shares"] = (m[mb + 2] - m[mb + 5]) * 0.01
         d[f"it{it}: solve"] = (m[mb + 3] - m[mb + 2]) * 0.01
         prev = mb + 3
     d["final apply + write-back"] = (m[63] - m[prev]) * 0.01
@@ -71,12 +73,6 @@ if m[48] and m[50] and m[63] > m[50]:
     print(f"final apply wg0: poses {(m[48] - m[mf]) * 0.01:.2f} us, depths "
           f"{(m[50] - m[49]) * 0.01:.2f} us, write-back + status {(m[63] - m[50]) * 0.01:.2f} us"
           f" (relevant edges {m[52]}, E entries {'in HBM' if m[53] & 1 else 'in LDS'})")
-
-# dense kernel (DPVO_BA_DENSE=1): workgroup 0's pass 0 of iteration 0
-if m[55] and m[58]:
-    print(f"dense wg0 pass0: (1) linearise {(m[56] - m[55]) * 0.01:.2f} us, (2) slots "
-          f"{(m[57] - m[56]) * 0.01:.2f} us, (3) block items {(m[58] - m[57]) * 0.01:.2f} us; "
-          f"passes {m[59]}, own edges {m[60]}, own patches {m[61]}")
 
 # per-workgroup spread (window kernel stamps [128 + 256 it + g] assembled,
 # [640 + 256 it + g] every partial seen), last call
@@ -96,12 +92,6 @@ if m[128] and len(m) >= 1664:
     print(f"setup done at {min(setup):.2f}..{max(setup):.2f} us (median "
           f"{statistics.median(setup):.2f}); it0 pre-reduction at {min(pre):.2f}..{max(pre):.2f} "
           f"(median {statistics.median(pre):.2f})")
-    if len(m) >= 2176 and m[1664]:  # dense kernel: linearised (pass 0) + own edges / patches
-        info = [(g, m[1920 + g] & 0xffff, m[1920 + g] >> 16,
-                 round((m[1664 + g] - m[1152 + g]) * 0.01, 2),
-                 round((m[1408 + g] - m[1664 + g]) * 0.01, 2)) for g in order[-8:] + order[:3]]
-        print("dense (g: own edges, own patches, setup->linearised us, linearised->pre-reduce us), "
-              "slowest 8 then fastest 3:", info)
     print("per workgroup (g: setup, pre-reduce, assembled, seen):",
           [(g, round(setup[g], 2), round(pre[g], 2), round((m[128 + g] - m[0]) * 0.01, 2),
             round((m[640 + g] - m[0]) * 0.01, 2)) for g in order[-8:]])

@@ -21,6 +21,27 @@ import torch  # noqa: E402
 
 from dpvo_amd import altcorr, fastba, synthetic  # noqa: E402
 
+def ba_phases(m, iters=2):
+    """Workgroup 0's phase table of the BA window kernel (as ba_window_phases.py)."""
+    d = {"BA kernel (marks)": m[63] - m[0], "setup": m[1] - m[0],
+         "  plan entries + counts": m[40] - m[0], "  scan": m[41] - m[40],
+         "  records": m[42] - m[41], "  patch values, edge ids, poses": m[43] - m[42],
+         "  per-edge inputs": m[1] - m[43]}
+    prev = 1
+    for it in range(iters):
+        mb = 2 + 8 * it
+        d[f"it{it}: (apply+) assemble"] = m[mb + 4] - m[prev]
+        d[f"it{it}: reduce + publish"] = m[mb] - m[mb + 4]
+        d[f"it{it}: wait partials"] = m[mb + 1] - m[mb]
+        d[f"it{it}: gather"] = m[mb + 2] - m[mb + 1]
+        d[f"it{it}:   last granules"] = m[mb + 5] - m[mb + 1]
+        d[f"it{it}:   sum shares"] = m[mb + 2] - m[mb + 5]
+        d[f"it{it}: solve"] = m[mb + 3] - m[mb + 2]
+        prev = mb + 3
+    d["final apply + write-back"] = m[63] - m[prev]
+    return {k: v * 0.01 for k, v in d.items()}
+
+
 PHASES = ["edge pass", "histogram", "local scan", "scatter", "block work", "rank + stores"]
 
 
@@ -67,13 +88,15 @@ def main():
         step(i)
     torch.cuda.synchronize()
     off = cb.plan_offsets(E, 1, G.F)
-    rows, phases = [], []
+    rows, phases, ba = [], [], []
     cb.set_marks(True)
     try:
         for i in range(args.steps):
             ws = step(i)
             torch.cuda.synchronize()
-            mk = cb.workspace_marks(ws, E, 1, G.F).cpu().numpy()[1664:].reshape(-1, 2)
+            allm = cb.workspace_marks(ws, E, 1, G.F).cpu().numpy()
+            ba.append(ba_phases(allm.tolist()))
+            mk = allm[1664:].reshape(-1, 2)
             b = ws.cpu().numpy().tobytes()
             st = np.frombuffer(b[off[4] + 64:off[4] + 64 + 72], np.int64)
             ph = np.diff(st[:7]) * 0.01
@@ -84,9 +107,12 @@ def main():
     m = np.median(np.array(phases), axis=0)
     plan_line = ("  plan shard 0 phases: " + ", ".join(f"{n} {x:.2f}" for n, x in zip(PHASES, m))
                  + f" us; total {m[:-1].sum():.2f} us; shader clock {m[-1]:.0f} MHz")
+    ba_lines = [f"  {k:34s} median {np.median([d[k] for d in ba]):6.2f} us" for k in ba[0]]
     if args.separate_insert:
         print(f"{args.config}: E={E}, frame insertion in its own launch")
         print(plan_line)
+        print("BA window kernel in the step (workgroup 0):")
+        print("\n".join(ba_lines))
         return
     nwg = int(max((r[:, 0] > 0).sum() for r in rows))
     roles = {"plan shards": range(0, nps), "edge order": range(nps, nps + 1),
@@ -115,6 +141,8 @@ def main():
         print(f"  {k:14s} first start {m[0]:5.2f}  median start {m[3]:5.2f}  last end {m[1]:5.2f}"
               f"  longest workgroup {m[2]:5.2f} us")
     print(plan_line)
+    print("BA window kernel in the step (workgroup 0):")
+    print("\n".join(ba_lines))
 
 
 if __name__ == "__main__":
