@@ -109,8 +109,8 @@ struct WArgs {
   const int64_t* kk;
   int E, P, num_poses, num_patches, t0, N, iters, NB, Sd, So, G;
   Plan plan;
-  double* part;      // [2][G][kPartPad] published partial blocks, by iteration parity (flag modes)
-  v4u* gran;         // [2][G][kGranPad] the same as 16-B granules (default mode)
+  double* part;      // [2][G][kPartPad] (workspace layout only: the exchange uses gran)
+  v4u* gran;         // [2][G][kGranPad] published partial blocks as 16-B granules, by iteration parity
   long long* flags;  // persistent [kFlagWords]
   float* ejg;        // [2][E][12] E entries by edge and iteration parity (fp32), HBM fallback
   int* status;       // [1] OR of status bits (workspace meta)
@@ -127,15 +127,6 @@ struct WArgs {
 
 __device__ __forceinline__ size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
 typedef double f64x2 __attribute__((ext_vector_type(2)));
-
-__device__ bool wait_flag(long long* p, long long target) {
-  const long long t0 = (long long)wall_clock64();
-  while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    __builtin_amdgcn_s_sleep(1);
-    if ((long long)wall_clock64() - t0 > kSpin) return false;
-  }
-  return true;
-}
 
 __device__ __forceinline__ void mark(const WArgs& A, int slot) {
   if (A.marks && blockIdx.x == 0 && threadIdx.x == 0) A.marks[slot] = (int64_t)wall_clock64();
@@ -1130,8 +1121,7 @@ __device__ __forceinline__ v4u granule(double v, unsigned long long key) {
 // fixed-order workgroup reduction of NA accumulators per thread -> out[0..NA)
 // (granule mode: gout = this workgroup's granule slot, tag its iteration tag)
 template <int NA>
-__device__ void reduce_acc(const double* acc, double* red, double* out, v4u* gout = nullptr,
-                           unsigned long long tag = 0) {
+__device__ void reduce_acc(const double* acc, double* red, v4u* gout, unsigned long long tag) {
   const int tid = threadIdx.x;
   // two rounds of 128 columns: red[v][col]
   if (tid >= 128) {
@@ -1160,18 +1150,10 @@ __device__ void reduce_acc(const double* acc, double* red, double* out, v4u* gou
   if (tid < NA) {
     const double* s = seg + 8 * tid;
     const double v = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-    if (gout) {
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc(gout, 0, 16 * kGranPad, kBufDword3);
-      __builtin_amdgcn_raw_buffer_store_b128(granule(v, tag), rs, 16 * tid, 0, kSc1);
-    } else {
-      __hip_atomic_store(out + tid, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(gout, 0, 16 * kGranPad, kBufDword3);
+    __builtin_amdgcn_raw_buffer_store_b128(granule(v, tag), rs, 16 * tid, 0, kSc1);  // needs no ordering
   }
-  // flag modes: the storing wave drains its stores before the workgroup
-  // barrier that precedes the flag (MI355X_MICROARCH.md "Valid forms":
-  // producer); granules need no ordering
-  if (!gout && tid < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
@@ -1631,8 +1613,6 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     // partials double-buffered by iteration parity: a workgroup can only reach
     // buffer it & 1 again (iteration it + 2) after every workgroup has published
     // iteration it + 1, i.e. after each finished reading iteration it's slots
-    double* const pbuf = A.part + (size_t)(it & 1) * A.G * kPartPad;
-    double* part = pbuf + (size_t)g * kPartPad;
     double* red = reinterpret_cast<double*>(L.region);
     const unsigned long long gkey = (unsigned long long)(epoch * 64 + it + 1) ^ A.salt;
     const unsigned gtag = (unsigned)gkey;
@@ -1644,11 +1624,11 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       assemble<1>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
       mark(A, mb + 4);
       if (A.marks && tid == 0 && it == 0 && g < 256) A.marks[1408 + g] = (int64_t)wall_clock64();
-      reduce_acc<27>(acc, red, part, gslot, gkey);
+      reduce_acc<27>(acc, red, gslot, gkey);
     } else {
       assemble<2>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
       if (A.marks && tid == 0 && it == 0 && g < 256) A.marks[1408 + g] = (int64_t)wall_clock64();
-      reduce_acc<36>(acc, red, part, gslot, gkey);
+      reduce_acc<36>(acc, red, gslot, gkey);
     }
     mark(A, mb + 0);
     if (A.marks && tid == 0 && it < 2 && g < 256)  // per-workgroup stamps (instrumentation)
