@@ -1416,8 +1416,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   // pass A1, thread per relevant patch, no global loads: record offsets, the
   // patch of every position, the final-depth writer
   int* rpo = reinterpret_cast<int*>(L.qu);  // first sorted position (until the first linearisation)
-  auto record = [&](int u, int kx, int po, unsigned m) {
-    const int c0 = cnt[u], c1 = (u + 1 < nuniq) ? cnt[u + 1] : tot;
+  auto record = [&](int u, int kx, int po, unsigned m, int c0, int c1) {
     const int ri = c0 >> 16, q0 = c0 & 0xffff, ne = (c1 - c0) & 0xffff;
     L.roff[ri] = q0;
     rpo[ri] = po;
@@ -1442,15 +1441,24 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     L.pkx[ri] = own ? kx : -1;
     return ri;
   };
-  auto live = [&](int u) {
-    return u < nuniq && cnt[u] != ((u + 1 < nuniq) ? cnt[u + 1] : tot);
-  };
+  // the prefix entries of the thread's patches are read in one batch (a live
+  // test per patch between the record stores waited for its own reads)
+  auto cnt_at = [&](int u) { return (u < nuniq) ? cnt[u] : tot; };
   bool lv0[kB];
+  {
+    int c0[kB], c1[kB];
 #pragma unroll
-  for (int r = 0; r < kB; r++) {
-    const int u = tid + r * kWT;
-    lv0[r] = nrel > 0 && live(min(u, nuniq - 1)) && u < nuniq;
-    if (lv0[r]) record(u, kx0[r], pa0[r], m0[r]);
+    for (int r = 0; r < kB; r++) {
+      const int u = min(tid + r * kWT, nuniq - 1);
+      c0[r] = cnt[u];
+      c1[r] = cnt_at(u + 1);
+    }
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      const int u = tid + r * kWT;
+      lv0[r] = nrel > 0 && u < nuniq && c0[r] != c1[r];
+      if (lv0[r]) record(u, kx0[r], pa0[r], m0[r], c0[r], c1[r]);
+    }
   }
   for (int u0 = tid + kB * kWT; u0 < nuniq && nrel > 0; u0 += kB * kWT) {
     int kx[kB], po[kB];
@@ -1462,10 +1470,17 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       po[r] = A.plan.poff[uc];
       msk[r] = A.plan.pmask[uc];
     }
+    int c0[kB], c1[kB];
+#pragma unroll
+    for (int r = 0; r < kB; r++) {
+      const int uc = min(u0 + r * kWT, nuniq - 1);
+      c0[r] = cnt[uc];
+      c1[r] = cnt_at(uc + 1);
+    }
 #pragma unroll
     for (int r = 0; r < kB; r++) {
       const int u = u0 + r * kWT;
-      if (u < nuniq && live(u)) record(u, kx[r], po[r], msk[r]);
+      if (u < nuniq && c0[r] != c1[r]) record(u, kx[r], po[r], msk[r], c0[r], c1[r]);
     }
   }
   if (tid == 0) L.roff[nrel] = nrp;
@@ -1525,7 +1540,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
 #pragma unroll
     for (int r = 0; r < kB; r++) {
       const int u = u0 + r * kWT, uc = min(u, nuniq - 1);
-      kx[r] = (u < nuniq && live(uc)) ? A.plan.pkk[uc] : -1;
+      kx[r] = (u < nuniq && cnt[uc] != cnt_at(uc + 1)) ? A.plan.pkk[uc] : -1;
     }
 #pragma unroll
     for (int r = 0; r < kB; r++) {
