@@ -177,7 +177,9 @@ __device__ __forceinline__ T row_sum(T v, int lpr) {
 __device__ __forceinline__ void residual64(const double* S, const double* y, const double* x,
                                            float* v, int N) {
   const int n = 6 * N, lpr = lanes_per_row(n);
-  const int t = threadIdx.x, row = t / lpr, part = t % lpr;
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));  // not loop-invariant for the caller (see wsolve)
+  const int row = t / lpr, part = t % lpr;
   double s0 = 0.0, s1 = 0.0;
   if (row < n) {
     const int i = row / 6, xr = row % 6;
@@ -336,7 +338,7 @@ __device__ __forceinline__ void ldl_sweeps(const float* A, const float* Z, int l
   }
 }
 
-// the same for a run-time N (12 <= N <= 16: larger windows than DPVO's)
+// the same for a run-time N (every N but 10 and 11)
 __device__ __forceinline__ void ldl_sweeps_rt(const float* A, const float* Z, int N, int lane,
                                            float& b0, float& b1) {
   const int n = 6 * N;
@@ -364,23 +366,19 @@ __device__ __forceinline__ void ldl_sweeps_rt(const float* A, const float* Z, in
 
 __device__ __forceinline__ void sweeps(const float* A, const float* Z, int N, int lane, float& b0,
                                        float& b1) {
+  // Unrolled for DPVO's window sizes only (N = 10: the fork's window of free
+  // poses, N = 11: cfg2).  Inside the window kernel's BA iteration loop the
+  // compiler hoists the per-lane row addresses and selects of every unrolled
+  // case before the loop (they are loop-invariant) and keeps them live in
+  // spilled registers: with all of N = 1..11 unrolled that was ~2000
+  // instructions (2.5 us) at the loop entry.  Other N take the loop form.
   switch (N) {
-#define DPVO_SWEEP_CASE(NN) \
-  case NN:                  \
-    ldl_sweeps<NN>(A, Z, lane, b0, b1); \
-    break;
-    DPVO_SWEEP_CASE(1)
-    DPVO_SWEEP_CASE(2)
-    DPVO_SWEEP_CASE(3)
-    DPVO_SWEEP_CASE(4)
-    DPVO_SWEEP_CASE(5)
-    DPVO_SWEEP_CASE(6)
-    DPVO_SWEEP_CASE(7)
-    DPVO_SWEEP_CASE(8)
-    DPVO_SWEEP_CASE(9)
-    DPVO_SWEEP_CASE(10)
-    DPVO_SWEEP_CASE(11)
-#undef DPVO_SWEEP_CASE
+    case 10:
+      ldl_sweeps<10>(A, Z, lane, b0, b1);
+      break;
+    case 11:
+      ldl_sweeps<11>(A, Z, lane, b0, b1);
+      break;
     default:
       ldl_sweeps_rt(A, Z, N, lane, b0, b1);
   }

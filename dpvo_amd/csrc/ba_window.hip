@@ -128,6 +128,16 @@ struct WArgs {
 __device__ __forceinline__ size_t al16(size_t v) { return (v + 15) & ~(size_t)15; }
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 
+// threadIdx.x through an empty asm: code inside the BA iteration loop that
+// derives from it is not loop-invariant, so the compiler does not hoist it
+// (addresses, masks of every phase) before the loop and keep it live across
+// the loop in spilled registers (2.5 us of hoisted work at the loop entry).
+__device__ __forceinline__ int opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 __device__ __forceinline__ void mark(const WArgs& A, int slot) {
   if (A.marks && blockIdx.x == 0 && threadIdx.x == 0) A.marks[slot] = (int64_t)wall_clock64();
 }
@@ -883,7 +893,7 @@ template <int MODE>  // 0: only Q, u (no free pose / N == 0); 1 diagonal block; 
 __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, double lam,
                          float fx, float fy, float cx, float cy, int par, double* acc) {
   constexpr int NA = (MODE == 1) ? 27 : (MODE == 2 ? 36 : 1);
-  const int tid = threadIdx.x, N = A.N;
+  const int tid = opaque_tid(), N = A.N;
   const unsigned ua = (unsigned)a, ub = (unsigned)b;
   double* pe = reinterpret_cast<double*>(L.region);  // [kChunk][14]: c, u, Ea[6], Eb[6]
 #pragma unroll
@@ -1122,7 +1132,7 @@ __device__ __forceinline__ v4u granule(double v, unsigned long long key) {
 // (granule mode: gout = this workgroup's granule slot, tag its iteration tag)
 template <int NA>
 __device__ void reduce_acc(const double* acc, double* red, v4u* gout, unsigned long long tag) {
-  const int tid = threadIdx.x;
+  const int tid = opaque_tid();
   // two rounds of 128 columns: red[v][col]
   if (tid >= 128) {
 #pragma unroll
@@ -1598,6 +1608,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
   // ---------------- iterations ----------------
   const double lam = (double)A.lmbda[0];
   for (int it = 0; it < A.iters; it++) {
+    const int tid = opaque_tid();  // (shadows the kernel's: see opaque_tid)
     const int mb = 2 + 8 * it;
     if (it > 0) {
       // ---- apply dX of iteration it-1: poses, then inverse depths ----
