@@ -44,7 +44,7 @@ constexpr int kMaxFree = 20;  // pose-block masks are 32-bit; lower S blocks of 
 constexpr int kPerThread = kMaxSetupE / kSetupThreads;
 constexpr int kCtlBytes = 512;
 constexpr int kSetupLds = 160 * 1024;
-constexpr int kMarks = 2176;  // [0, 128) phases; window kernel per workgroup: [128 + 256 it + g] assembled, [640 + 256 it + g] all partials seen, [1152 + g] setup, [1408 + g] it 0 pre-reduction; fused reproject + plan + insert launch: [1664 + 2b] / [1665 + 2b] start / end of workgroup b
+constexpr int kMarks = 2432;  // [0, 128) phases; window kernel per workgroup: [128 + 256 it + g] assembled, [640 + 256 it + g] all partials seen, [1152 + g] setup, [1408 + g] it 0 pre-reduction; fused reproject + plan + insert launch: [1664 + 2b] / [1665 + 2b] start / end of workgroup b; window kernel [2176 + g] end of workgroup g
 constexpr int kLaunchMarks = 1664;
 constexpr int kNoPose = 31;
 constexpr int kEC = 16;  // doubles per position record of E terms

@@ -115,7 +115,7 @@ struct WArgs {
   float* ejg;        // [2][E][12] E entries by edge and iteration parity (fp32), HBM fallback
   int* status;       // [1] OR of status bits (workspace meta)
   int* sink;         // caller's sticky status word (dpvo_ba_set_status_sink) or null
-  int64_t* marks;    // [2176] wall-clock stamps (instrumentation, dpvo_ba_set_marks): [0, 64)
+  int64_t* marks;    // [2432] wall-clock stamps (instrumentation, dpvo_ba_set_marks): [0, 64)
                      // phases of workgroup 0, [128 + 256 it + g] / [640 + 256 it + g] per
                      // workgroup assembled / all partials seen, [1152 + g] setup done,
                      // [1408 + g] iteration 0 assembled (before the reduction); null on
@@ -1888,6 +1888,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
       __hip_atomic_store(&A.flags[kEpochWord], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       mark(A, 63);
     }
+    if (A.marks && g < 256) A.marks[2176 + g] = (int64_t)wall_clock64();  // workgroup end
   }
 }
 

@@ -253,7 +253,7 @@ void ba_forward_planned(torch::Tensor ws, torch::Tensor poses, torch::Tensor pat
   track_status(ws, poses, E, t0, t1);
 }
 
-// Same call; returns the 2176 phase marks (100 MHz ticks: [0, 128) phases; window kernel
+// Same call; returns the 2432 phase marks (100 MHz ticks: [0, 128) phases; window kernel
 // [128 + 256 it + g] / [640 + 256 it + g] per-workgroup assembled / partials seen, [1152 + g]
 // setup done, [1408 + g] iteration 0 assembled before its reduction) followed by the
 // multi-kernel path's per-workgroup marks.
@@ -272,7 +272,7 @@ torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
     throw;
   }
   check_status(dpvo_ba_set_marks(0), "cuda_ba.forward_marks");
-  auto out = torch::zeros({2176}, poses.options().dtype(torch::kInt64));
+  auto out = torch::zeros({2432}, poses.options().dtype(torch::kInt64));
   if (!ws.defined()) return out;
   check_status(dpvo_ba_phase_marks(ws.data_ptr(), ii.numel(), t0, t1, out.data_ptr<int64_t>(),
                                    current_stream()),
@@ -288,7 +288,7 @@ torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
 
 // The marks a workspace holds (after launches made with set_marks(true)).
 torch::Tensor ba_workspace_marks(torch::Tensor ws, int64_t E, int t0, int t1) {
-  auto out = torch::zeros({2176}, ws.options().dtype(torch::kInt64));
+  auto out = torch::zeros({2432}, ws.options().dtype(torch::kInt64));
   check_status(dpvo_ba_phase_marks(ws.data_ptr(), (int)E, t0, t1, out.data_ptr<int64_t>(),
                                    current_stream()),
                "cuda_ba.workspace_marks");
@@ -1065,7 +1065,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_marks", [](bool on) { check_status(dpvo_ba_set_marks(on ? 1 : 0), "set_marks"); },
         "stamp wall-clock marks into the BA workspace (instrumentation)");
   m.def("workspace_marks", &ba_workspace_marks,
-        "the 2176 marks of a workspace ([1664 + 2b] / [1665 + 2b]: fused launch workgroup b)");
+        "the 2432 marks of a workspace ([1664 + 2b] / [1665 + 2b]: fused launch workgroup b)");
   m.def("forward_dx", &ba_forward_dx, "forward; returns the last iteration's dX [N, 6] (fp64)");
   m.def("last_dx", &ba_last_dx, "dX [N, 6] of the last iteration of a planned forward on ws");
   m.def("reproject_ordered_plan", &ba_reproject_ordered_plan,

@@ -92,6 +92,11 @@ if m[128] and len(m) >= 1664:
     print(f"setup done at {min(setup):.2f}..{max(setup):.2f} us (median "
           f"{statistics.median(setup):.2f}); it0 pre-reduction at {min(pre):.2f}..{max(pre):.2f} "
           f"(median {statistics.median(pre):.2f})")
+    if len(m) >= 2432 and m[2176]:
+        ends = [(m[2176 + g] - m[0]) * 0.01 for g in range(G)]
+        print(f"workgroup ends at {min(ends):.2f}..{max(ends):.2f} us (median "
+              f"{statistics.median(ends):.2f}; workgroup 0 at {(m[63] - m[0]) * 0.01:.2f}); "
+              f"last workgroups {sorted(range(G), key=lambda g: ends[g])[-5:]}")
     print("per workgroup (g: setup, pre-reduce, assembled, seen):",
           [(g, round(setup[g], 2), round(pre[g], 2), round((m[128 + g] - m[0]) * 0.01, 2),
             round((m[640 + g] - m[0]) * 0.01, 2)) for g in order[-8:]])
