@@ -613,18 +613,29 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
             const float4 c1 = __builtin_bit_cast(float4, B[2 * t + 1]);
             const float x[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
             f16x8 bh, bl;
+#ifdef CORR_DIAG_NO_CONV  // diagnostic builds only: the tile's two 16-B pieces taken as
+                          // ready f16 halves (the loads of a pre-split pyramid, no conversion)
+            (void)x;
+            bh = __builtin_bit_cast(f16x8, B[2 * t]);
+            bl = __builtin_bit_cast(f16x8, B[2 * t + 1]);
+#else
 #pragma unroll
             for (int j = 0; j < 8; j++) {
               const _Float16 hv = (_Float16)x[j];
               bh[j] = hv;
               bl[j] = (_Float16)(x[j] - (float)hv);
             }
+#endif
             acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah[t], bh, acc0, 0, 0, 0);
             acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah[t], bl, acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Alds[t * kWave + lane], bh, acc1, 0, 0, 0);
           }
+#ifdef CORR_DIAG_NO_CONV
+          const bool fin = true;
+#else
           const bool fin = __builtin_isfinite(acc0[0] + acc0[1] + acc0[2] + acc0[3] + acc1[0] +
                                               acc1[1] + acc1[2] + acc1[3]);
+#endif
           bad = bad || __builtin_amdgcn_ballot_w64(!fin) != 0;
         }
       };
