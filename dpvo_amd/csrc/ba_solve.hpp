@@ -281,8 +281,14 @@ __device__ __forceinline__ const float* fwd_row(const float* A, const float* Z, 
 __device__ __forceinline__ const float* bwd_col(const float* Z, int i, int x, int k) {
   return Z + 36 * lblk(k, (i < k) ? i : 0) + x;
 }
+// packed fp32 (v_pk_fma_f32: two products per instruction): (even, odd)
+// partial sums, then one add
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float dot6(const float l[6], const float v[6]) {
-  return (l[0] * v[0] + l[1] * v[1] + l[2] * v[2]) + (l[3] * v[3] + l[4] * v[4] + l[5] * v[5]);
+  f32x2 s = f32x2{l[0], l[1]} * f32x2{v[0], v[1]};
+  s = __builtin_elementwise_fma(f32x2{l[2], l[3]}, f32x2{v[2], v[3]}, s);
+  s = __builtin_elementwise_fma(f32x2{l[4], l[5]}, f32x2{v[4], v[5]}, s);
+  return s.x + s.y;
 }
 
 template <int NN>
@@ -441,18 +447,14 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
           ld_row(s.A + 36 * lblk(ia, k) + 6 * xa, a);
           ld_row(s.A + 36 * lblk(ia, c1) + 6 * xa, v0);
 #pragma unroll
-          for (int z = 0; z < 6; z++)
-#pragma unroll
-            for (int q = 0; q < 6; q++) v0[z] -= a[q] * B[6 * z + q];
+          for (int z = 0; z < 6; z++) v0[z] -= dot6(a, B + 6 * z);
         }
         if (nr > 64) {
           float a[6];
           ld_row(s.A + 36 * lblk(ib, k) + 6 * xb, a);
           ld_row(s.A + 36 * lblk(ib, c1) + 6 * xb, v1);
 #pragma unroll
-          for (int z = 0; z < 6; z++)
-#pragma unroll
-            for (int q = 0; q < 6; q++) v1[z] -= a[q] * B[6 * z + q];
+          for (int z = 0; z < 6; z++) v1[z] -= dot6(a, B + 6 * z);
         }
         WSTAMP_DBG(56);
         // pivot rows (lanes 0-5) to every lane through LDS: the rows go to the
