@@ -12,7 +12,8 @@
 //     written by lanes 0-5, and panel column k+1 formed from the rows still
 //     in registers -- one LDS round trip per step.  Waves 1-3 meanwhile apply
 //     panel k to the rest of the trailing matrix.  One workgroup barrier per
-//     block step.
+//     block step.  The chain is instruction issue on one wave, so its 6-term
+//     dots (column update, sweeps) are packed fp32 (v_pk_fma_f32).
 //   * The factor is turned into block LDL^T form, A = Lt D Lt^T with
 //     Lt_ik = L_ik Linv_kk and D_k^-1 = Linv_kk^T Linv_kk (ldl_task, by wave 3
 //     while the trailing update leaves it idle), so a block step of the
@@ -457,20 +458,16 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
           for (int z = 0; z < 6; z++) v1[z] -= dot6(a, B + 6 * z);
         }
         WSTAMP_DBG(56);
-        // pivot rows (lanes 0-5) to every lane through LDS: the rows go to the
-        // pivot block (only Linv is kept of it; D^-1 overwrites it later)
-        float* pv = s.A + 36 * lblk(c1, c1);
-        if (lane < 6) st_row(pv + 6 * lane, v0);
-        wave_lds_sync();
         float m[6][6], L[6][6], ri[6];
-        {
-          float P[36];
-          ld_blk(pv, P);
+        // the 21 lower pivot entries (row r = lane r's v0) to every lane by
+        // v_readlane: 33.1k vs 34.9k cycles per N = 11 solve against a store
+        // of the rows to LDS, a wave LDS fence and a 144-B block load (nothing
+        // else reads the updated pivot rows: only Linv is kept of the block)
 #pragma unroll
-          for (int r = 0; r < 6; r++)
+        for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int c = 0; c <= r; c++) m[r][c] = P[6 * r + c];
-        }
+          for (int c = 0; c <= r; c++)
+            m[r][c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v0[c]), r));
         WSTAMP_DBG(57);
         const bool ok = chol6_m(m, L, ri);
         WSTAMP_DBG(58);
