@@ -51,6 +51,8 @@ __host__ __device__ constexpr size_t wsolve_bytes(int N) {
          sizeof(double) * 2 * 6 * (size_t)N;
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_fma_f32)
+
 // Wide LDS accesses: a 6x6 block is 144 B (9 x 16 B) at a 16-B aligned
 // base, a row 24 B (3 x 8 B).  Few, wide DS instructions keep each step
 // inside the 15 outstanding LDS requests a wave may have.
@@ -150,14 +152,13 @@ __device__ __forceinline__ void row2_sub_abt(float* out, const float* arow, cons
   ld_blk(Bp, B);
 #pragma unroll
   for (int z = 0; z < 6; z++) {
-    float s0 = o0[z], s1 = o1[z];
+    // rows x and x + 1 as one packed pair (v_pk_fma_f32), B broadcast
+    f32x2 s = f32x2{o0[z], o1[z]};
 #pragma unroll
-    for (int q = 0; q < 6; q++) {
-      s0 -= a0[q] * B[6 * z + q];
-      s1 -= a1[q] * B[6 * z + q];
-    }
-    o0[z] = s0;
-    o1[z] = s1;
+    for (int q = 0; q < 6; q++)
+      s = __builtin_elementwise_fma(f32x2{-a0[q], -a1[q]}, f32x2{B[6 * z + q], B[6 * z + q]}, s);
+    o0[z] = s.x;
+    o1[z] = s.y;
   }
   st_row(out, o0);
   st_row(out + 6, o1);
@@ -184,6 +185,9 @@ __device__ __forceinline__ void residual64(const double* S, const double* y, con
   double s0 = 0.0, s1 = 0.0;
   if (row < n) {
     const int i = row / 6, xr = row % 6;
+    // unrolled: the loads of later blocks issue before the fp64 FMA chains of
+    // the first (one LDS wait for several blocks instead of one per block)
+#pragma unroll 4
     for (int j = part; j < N; j += lpr) {
       const double* b = (i >= j) ? S + 36 * lblk(i, j) + 6 * xr : S + 36 * lblk(j, i) + xr;
       const int st = (i >= j) ? 1 : 6;
@@ -284,7 +288,6 @@ __device__ __forceinline__ const float* bwd_col(const float* Z, int i, int x, in
 }
 // packed fp32 (v_pk_fma_f32: two products per instruction): (even, odd)
 // partial sums, then one add
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float dot6(const float l[6], const float v[6]) {
   f32x2 s = f32x2{l[0], l[1]} * f32x2{v[0], v[1]};
   s = __builtin_elementwise_fma(f32x2{l[2], l[3]}, f32x2{v[2], v[3]}, s);
