@@ -889,9 +889,13 @@ __device__ __forceinline__ void pose_of(const WArgs& A, const WL& L, unsigned sl
   }
 }
 
+// nact (out): the threads [0, nact) are the only ones whose acc can be
+// nonzero (thread t takes edge q0 + t of a chunk and patch pa + t)
 template <int MODE>  // 0: only Q, u (no free pose / N == 0); 1 diagonal block; 2 off-diagonal
 __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, double lam,
-                         float fx, float fy, float cx, float cy, int par, double* acc) {
+                         float fx, float fy, float cx, float cy, int par, double* acc,
+                         int& nact) {
+  nact = 0;
   constexpr int NA = (MODE == 1) ? 27 : (MODE == 2 ? 36 : 1);
   const int tid = opaque_tid(), N = A.N;
   const unsigned ua = (unsigned)a, ub = (unsigned)b;
@@ -911,6 +915,7 @@ __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, do
       pb = lo;
     }
     const int q0 = L.roff[pa], q1 = L.roff[pb];
+    nact = max(nact, min(max(q1 - q0, pb - pa), kWT));
     // pass 1: thread per edge
     for (int q = q0 + tid; q < q1; q += kWT) {
       const unsigned c = L.ec[q];
@@ -1131,17 +1136,25 @@ __device__ __forceinline__ v4u granule(double v, unsigned long long key) {
 // fixed-order workgroup reduction of NA accumulators per thread -> out[0..NA)
 // (granule mode: gout = this workgroup's granule slot, tag its iteration tag)
 template <int NA>
-__device__ void reduce_acc(const double* acc, double* red, v4u* gout, unsigned long long tag) {
+__device__ void reduce_acc(const double* acc, double* red, v4u* gout, unsigned long long tag,
+                           int nact) {
   const int tid = opaque_tid();
-  // two rounds of 128 columns: red[v][col]
-  if (tid >= 128) {
+  // two rounds of 128 columns: red[v][col]; one when only threads below 128
+  // hold nonzero sums (nact <= 128: cfg2's workgroups have ~100 relevant
+  // edges), saving a barrier and the upper half's stores and adds
+  if (nact > 128) {
+    if (tid >= 128) {
 #pragma unroll
-    for (int v = 0; v < NA; v++) red[v * 128 + tid - 128] = acc[v];
-  }
-  __syncthreads();
-  if (tid < 128) {
+      for (int v = 0; v < NA; v++) red[v * 128 + tid - 128] = acc[v];
+    }
+    __syncthreads();
+    if (tid < 128) {
 #pragma unroll
-    for (int v = 0; v < NA; v++) red[v * 128 + tid] += acc[v];
+      for (int v = 0; v < NA; v++) red[v * 128 + tid] += acc[v];
+    }
+  } else if (tid < 128) {
+#pragma unroll
+    for (int v = 0; v < NA; v++) red[v * 128 + tid] = acc[v];
   }
   __syncthreads();
   // 8 segments of 16 columns per value, 4 independent partial sums each
@@ -1636,6 +1649,7 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     }
     // ---- linearise + assemble this workgroup's block ----
     double acc[36];
+    int nact = kWT;  // threads that can hold nonzero acc (assemble)
     // partials double-buffered by iteration parity: a workgroup can only reach
     // buffer it & 1 again (iteration it + 2) after every workgroup has published
     // iteration it + 1, i.e. after each finished reading iteration it's slots
@@ -1645,16 +1659,16 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     v4u* const gbuf = A.gran + (size_t)(it & 1) * A.G * kGranPad;
     v4u* const gslot = gbuf + (size_t)g * kGranPad;
     if (NB == 0) {
-      assemble<0>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
+      assemble<0>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc, nact);
     } else if (diag) {
-      assemble<1>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
+      assemble<1>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc, nact);
       mark(A, mb + 4);
       if (A.marks && tid == 0 && it == 0 && g < 256) A.marks[1408 + g] = (int64_t)wall_clock64();
-      reduce_acc<27>(acc, red, gslot, gkey);
+      reduce_acc<27>(acc, red, gslot, gkey, nact);
     } else {
-      assemble<2>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc);
+      assemble<2>(A, L, nrel_e, a, b, lam, fx, fy, cx, cy, it & 1, acc, nact);
       if (A.marks && tid == 0 && it == 0 && g < 256) A.marks[1408 + g] = (int64_t)wall_clock64();
-      reduce_acc<36>(acc, red, gslot, gkey);
+      reduce_acc<36>(acc, red, gslot, gkey, nact);
     }
     mark(A, mb + 0);
     if (A.marks && tid == 0 && it < 2 && g < 256)  // per-workgroup stamps (instrumentation)
