@@ -1464,9 +1464,16 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     L.pkx[ri] = own ? kx : -1;
     return ri;
   };
-  // the prefix entries of the thread's patches are read in one batch (a live
-  // test per patch between the record stores waited for its own reads)
+  // (1) the prefix entries of the thread's patches are read in one batch (a
+  // live test per patch between the record stores waited for its own reads)
+  // and each live patch leaves (u | mask << 16, kx, first position) at its
+  // record index; (2) after a barrier, a thread per record builds it.  A
+  // workgroup's few relevant patches are scattered over the kB slots of all
+  // threads, so record() run per slot issued its ~200 instructions kB times
+  // per wave; per record index it runs once.
   auto cnt_at = [&](int u) { return (u < nuniq) ? cnt[u] : tot; };
+  static_assert(kWMaxE <= 65536 && kWMaxN <= 16, "patch index and pose mask packed in 16 bits each");
+  int* dl = rpo + (nrel + 1);  // [nrel][3] scratch in qu's space past rpo (qu: 4 ints per record)
   bool lv0[kB];
   {
     int c0[kB], c1[kB];
@@ -1480,7 +1487,12 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     for (int r = 0; r < kB; r++) {
       const int u = tid + r * kWT;
       lv0[r] = nrel > 0 && u < nuniq && c0[r] != c1[r];
-      if (lv0[r]) record(u, kx0[r], pa0[r], m0[r], c0[r], c1[r]);
+      if (lv0[r]) {
+        int* d = dl + 3 * (c0[r] >> 16);
+        d[0] = (int)((unsigned)u | (m0[r] << 16));
+        d[1] = kx0[r];
+        d[2] = pa0[r];
+      }
     }
   }
   for (int u0 = tid + kB * kWT; u0 < nuniq && nrel > 0; u0 += kB * kWT) {
@@ -1503,8 +1515,20 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
 #pragma unroll
     for (int r = 0; r < kB; r++) {
       const int u = u0 + r * kWT;
-      if (u < nuniq && c0[r] != c1[r]) record(u, kx[r], po[r], msk[r], c0[r], c1[r]);
+      if (u < nuniq && c0[r] != c1[r]) {
+        int* d = dl + 3 * (c0[r] >> 16);
+        d[0] = (int)((unsigned)u | (msk[r] << 16));
+        d[1] = kx[r];
+        d[2] = po[r];
+      }
     }
+  }
+  __syncthreads();
+  for (int t = tid; t < nrel; t += kWT) {
+    const int* d = dl + 3 * t;
+    const unsigned um = (unsigned)d[0];
+    const int u = (int)(um & 0xffffu);
+    record(u, d[1], d[2], um >> 16, cnt[u], cnt_at(u + 1));
   }
   if (tid == 0) L.roff[nrel] = nrp;
   __syncthreads();
