@@ -1524,29 +1524,26 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     }
   }
   __syncthreads();
+  // the record's patch values [0][1][1], [1][1][1], [2][1][1], [2][0][0]
+  // (ba_cuda.cu:282-285, :225) are loaded first: their round trip overlaps
+  // the record's LDS work
+  const int c11 = P + 1;
   for (int t = tid; t < nrel; t += kWT) {
     const int* d = dl + 3 * t;
     const unsigned um = (unsigned)d[0];
-    const int u = (int)(um & 0xffffu);
-    record(u, d[1], d[2], um >> 16, cnt[u], cnt_at(u + 1));
+    const int u = (int)(um & 0xffffu), kx = d[1];
+    const float* pk = A.patches + (size_t)kx * 3 * PP;
+    const float v0 = pk[c11], v1 = pk[PP + c11], v2 = pk[2 * PP + c11], v3 = pk[2 * PP];
+    record(u, kx, d[2], um >> 16, cnt[u], cnt_at(u + 1));
+    L.nxy[t] = make_float2((v0 - cx) / fx, (v1 - cy) / fy);
+    L.dep[t] = v2;
+    L.dbase[t] = v3;  // patch_retr_kernel reads [2][0][0] (:225)
   }
   if (tid == 0) L.roff[nrel] = nrp;
   __syncthreads();
   mark(A, 42);
-  // pass A2 + pass B, second round trip: the values of this thread's first-batch
-  // patches, the edge ids of its first kB relevant edges and the pose table,
-  // all issued before any is used
-  // patch values: [0][1][1], [1][1][1], [2][1][1], [2][0][0] (ba_cuda.cu:282-285, :225)
-  float cv[kB][4];
-  const int c11 = P + 1;
-#pragma unroll
-  for (int r = 0; r < kB; r++) {
-    const float* pk = A.patches + (size_t)(lv0[r] ? kx0[r] : 0) * 3 * PP;
-    cv[r][0] = pk[c11];
-    cv[r][1] = pk[PP + c11];
-    cv[r][2] = pk[2 * PP + c11];
-    cv[r][3] = pk[2 * PP];
-  }
+  // pass B, second round trip: the edge ids of this thread's first kB
+  // relevant edges and the pose table, all issued before any is used
   int ev0[kB];
 #pragma unroll
   for (int r = 0; r < kB; r++) {
@@ -1564,42 +1561,12 @@ __global__ void __launch_bounds__(kWT) ba_window_kernel(WArgs A) {
     const int gp = (sl < N) ? t0w + sl : fmin + (sl - N);
     pv[r] = A.poses[7 * (size_t)min(max(gp, 0), A.num_poses - 1) + min(c, 6)];
   }
-  auto patch_vals = [&](int u, const float* v) {
-    const int ri = cnt[u] >> 16;
-    L.nxy[ri] = make_float2((v[0] - cx) / fx, (v[1] - cy) / fy);
-    L.dep[ri] = v[2];
-    L.dbase[ri] = v[3];  // patch_retr_kernel reads [2][0][0] (:225)
-  };
-#pragma unroll
-  for (int r = 0; r < kB; r++)
-    if (lv0[r]) patch_vals(tid + r * kWT, cv[r]);
 #pragma unroll
   for (int r = 0; r < kPr; r++) {
     const int k = tid + r * kWT, sl = k >> 3, c = k & 7;
     const int gp = (sl < N) ? t0w + sl : fmin + (sl - N);
     const bool ok = c < 7 && gp >= 0 && gp < A.num_poses && (sl < N || fmin != 0x7fffffff);
     L.pose[k] = ok ? pv[r] : ((c == 6) ? 1.0f : 0.0f);
-  }
-  // patches past the first batch
-  for (int u0 = tid + kB * kWT; u0 < nuniq && nrel > 0; u0 += kB * kWT) {
-    float cw[kB][4];
-    int kx[kB];
-#pragma unroll
-    for (int r = 0; r < kB; r++) {
-      const int u = u0 + r * kWT, uc = min(u, nuniq - 1);
-      kx[r] = (u < nuniq && cnt[uc] != cnt_at(uc + 1)) ? A.plan.pkk[uc] : -1;
-    }
-#pragma unroll
-    for (int r = 0; r < kB; r++) {
-      const float* pk = A.patches + (size_t)max(kx[r], 0) * 3 * PP;
-      cw[r][0] = pk[c11];
-      cw[r][1] = pk[PP + c11];
-      cw[r][2] = pk[2 * PP + c11];
-      cw[r][3] = pk[2 * PP];
-    }
-#pragma unroll
-    for (int r = 0; r < kB; r++)
-      if (kx[r] >= 0) patch_vals(u0 + r * kWT, cw[r]);
   }
   mark(A, 43);
   // pass B, thread per relevant edge: slots, edge index, target/weight (the
