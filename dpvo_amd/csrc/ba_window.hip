@@ -908,9 +908,13 @@ __device__ void assemble(const WArgs& A, const WL& L, int nrel, int a, int b, do
     {
       int lo = pa + 1, hi = nrel;  // largest pb with roff[pb] - roff[pa] <= kChunk
       const int base = L.roff[pa];
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (L.roff[mid] - base <= kChunk) lo = mid; else hi = mid - 1;
+      if (L.roff[nrel] - base <= kChunk) {
+        lo = nrel;  // the rest fits (cfg2: every edge in one chunk): no search
+      } else {
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (L.roff[mid] - base <= kChunk) lo = mid; else hi = mid - 1;
+        }
       }
       pb = lo;
     }
