@@ -36,9 +36,9 @@ namespace dpvo {
 namespace bad {
 
 struct WSolve {
-  const double* S;  // [NB][36] damped S (fp64)
+  const double* S;  // [NB][36] damped S (fp64), 16-B aligned (read in pairs)
   const double* y;  // [n]
-  float* A;         // [NB][36]
+  float* A;         // [NB][36], 8-B aligned
   float* Z;         // [NB][36]
   float* v0;        // [n] unused (layout compatibility)
   float* v1;        // [n] fp32 work vector
@@ -414,7 +414,11 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
   const int NB = N * (N + 1) / 2, n = 6 * N;
   wstamp(st, 0);
   if (wid == 0) __builtin_amdgcn_s_setprio(3);
-  for (int k = tid; k < 36 * NB; k += blockDim.x) s.A[k] = (float)s.S[k];
+  // pairs: one 16-B read and one 8-B write per two entries (S 16-B, A 8-B aligned)
+  for (int k = tid; k < 18 * NB; k += blockDim.x) {
+    const double2 v = reinterpret_cast<const double2*>(s.S)[k];
+    reinterpret_cast<float2*>(s.A)[k] = make_float2((float)v.x, (float)v.y);
+  }
   for (int k = tid; k < n; k += blockDim.x) s.v1[k] = (float)s.y[k];
   if (tid == 0) *fail = 0;
   __syncthreads();
