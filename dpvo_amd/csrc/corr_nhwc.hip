@@ -705,6 +705,394 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   CORR_STAMP_RT(13);
 }
 
+// ---------------------------------------------------------------------------
+// corr_nhwc_lvl_kernel: fp32 features, exact fp32 products
+// (v_mfma_f32_16x16x4_f32), one wave per (edge, pyramid level) unit.
+//
+// What bounds A-CORR is the vector-memory path, not the matrix cores: the
+// loads alone of the per-edge kernel's B layout (16 box pixels x 64 B per
+// global_load_dwordx4 = 16 half-used 128-B lines per KiB) take 46.6 us at
+// cfg2, the same bytes as whole lines (8 pixels x 128 B per instruction)
+// 28.0 us (scripts/micro/load_pattern.hip).  So the box tiles are loaded as
+// whole lines and turned into the MFMA B layout through a 2-KiB LDS stage per
+// wave (one 32-channel quarter of the tile's 16 pixels at a time, XOR-swizzled
+// so both the stage writes and the B-fragment reads are conflict-free).
+// Units: one wave per (edge, level) (8192 at cfg2) puts 4 waves on a SIMD
+// instead of the per-edge kernel's 2; every wave runs TWO units, level l of
+// edge A and level L-1-l of edge B (the fine and the coarse levels pair up:
+// 7 + 4 and 6 + 5 tiles at cfg2), so the whole grid is resident at once
+// (4096 waves on 1024 SIMDs) with no second-round tail.  The waves are
+// independent (no barrier); each builds its unit's A fragments (the gmap
+// patch, 32 registers) and writes its level's slice of the edge's [nout][L]
+// output block.
+// ---------------------------------------------------------------------------
+constexpr int kLvlMaxTiles = 10;                   // box up to 160 pixels on the matrix path
+constexpr int kLvlBoxStride = 16 * kLvlMaxTiles + 4;
+constexpr int kLvlStage = 16 * 128;                // bytes: 16 pixels x one 128-B quarter
+
+struct LvlGeom {
+  int x0[kNpMax], y0[kNpMax];
+  float dx[kNpMax], dy[kNpMax];
+};
+// per wave: G [np][kLvlBoxStride] floats, the stage, the geometry
+__host__ __device__ inline int corr_lvl_wave_bytes(int np) {
+  return (int)(sizeof(float) * np * kLvlBoxStride + kLvlStage + sizeof(LvlGeom));
+}
+
+#ifndef LVL_STAMP
+#define LVL_STAMP_INIT
+#define LVL_STAMP(k)
+#endif
+// RAW9: p = 3, R = 3 (DPVO) as compile-time constants; otherwise run-time np, R
+template <int RING, bool RAW9>
+__global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_eu(RING > 2 ? 3 : 4)))
+    corr_nhwc_lvl_kernel(const float* __restrict__ fmap1, NhwcLevels lv, int L,
+                         const float* __restrict__ coords, const int64_t* __restrict__ ii,
+                         const int64_t* __restrict__ jj, int B, int M, int np_, int N1, int N2,
+                         int R_, const int* __restrict__ order, float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int np = RAW9 ? 9 : np_, R = RAW9 ? 3 : R_;
+  const int w = wave_uniform(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
+  const int C = kNhwcC, D = 2 * R + 2, Dp = D - 1, nout = Dp * Dp * np;
+  LVL_STAMP_INIT;
+  char* wl = reinterpret_cast<char*>(smem) + (size_t)w * corr_lvl_wave_bytes(np);
+  float* G = reinterpret_cast<float*>(wl);
+  char* stage = wl + sizeof(float) * np * kLvlBoxStride;
+  LvlGeom* geo = reinterpret_cast<LvlGeom*>(stage + kLvlStage);
+  const int ai = lane & 15, aq = lane >> 4;
+
+  // edge positions of this workgroup: with an order (B == 1, XCD-aware) XCD
+  // x = blockIdx % 8 takes the x-th eighth of the edges grouped by target
+  // frame, a workgroup two positions of it half an eighth apart
+  const int nE = B * M;
+  const int per = order ? (M + 7) / 8 : nE, half = (per + 1) / 2;
+  const int x8 = order ? (int)(blockIdx.x % 8) : 0, j8 = order ? (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  if (j8 >= half) return;
+
+  // ---- one (edge position p, level lev) unit
+  auto run_unit = [&](int p, int lev) __attribute__((always_inline)) {
+    LVL_STAMP(0);
+    const int edge = order ? wave_uniform(order[p]) : p;
+    const int b = edge / M, m = edge % M;
+    const int ix = wave_uniform((int)ii[m]), jx = wave_uniform((int)jj[m]);
+    const bool idx_ok = ix >= 0 && ix < N1 && jx >= 0 && jx < N2;
+
+    // the gmap patch [C][np] (whole lines, 16 B per lane), staged through G
+    // once the first box tiles are in flight
+    constexpr int kPA = (kNhwcC * (RAW9 ? 9 : kNpMax) / 4 + kWave - 1) / kWave;
+    const int n16 = C * np / 4;
+    u32x4 pa[kPA];
+    {
+      const float* f1 = fmap1 + ((size_t)b * N1 + (idx_ok ? ix : 0)) * C * np;
+#pragma unroll
+      for (int r = 0; r < kPA; r++)
+        pa[r] = reinterpret_cast<const u32x4*>(f1)[min(lane + kWave * r, n16 - 1)];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // the geometry waits for the coordinates only
+
+    // the edge's coordinates: RAW9 by scalar loads (uniform address: the
+    // scalar cache, not the vector-memory queue the tile loads keep full)
+    float cx = 0.f, cy = 0.f;  // lane k < np: patch pixel k (level-1 pixels)
+    if constexpr (RAW9) {
+      const float* cp = coords + ((size_t)b * M + m) * 18;
+      float c[18];
+#pragma unroll
+      for (int j = 0; j < 18; j++) c[j] = cp[j];
+#pragma unroll
+      for (int j = 0; j < 9; j++) {
+        cx = (lane == j) ? c[j] : cx;
+        cy = (lane == j) ? c[9 + j] : cy;
+      }
+    } else {
+      const float cv = (lane < 2 * np) ? coords[((size_t)b * M + m) * 2 * np + lane] : 0.f;
+      cx = __shfl(cv, min(ai, np - 1), kWave);
+      cy = __shfl(cv, np + min(ai, np - 1), kWave);
+    }
+
+    // geometry of the level: lane k < np takes patch pixel k (floor / frac),
+    // row (16-lane) min / max scans by DPP give the box
+    const int H2 = LV_SEL(H2, lev), W2 = LV_SEL(W2, lev);
+    int xlo, ylo, bw, bh;
+    bool inner;  // box not clamped to the map: every tap of every window is in it
+    int kb[9];   // RAW9, per patch pixel k (wave-uniform): window origin in G ...
+    float w00[9], w01[9], w10[9], w11[9];  // ... and the bilinear weights
+    {
+      const bool act = lane < np;
+      const float sc = LV_SEL(scale, lev);
+      const bool pow2 = (__float_as_uint(sc) & 0x7fffffu) == 0u;  // x / 2^k == x * 2^-k
+      const float rs = 1.0f / sc;
+      const float x = pow2 ? cx * rs : cx / sc, y = pow2 ? cy * rs : cy / sc;
+      const int xf = ifloor_safe(x), yf = ifloor_safe(y);
+      const float dx = x - floorf(x), dy = y - floorf(y);  // correlation_kernel.cu:262
+      if (act) {
+        geo->x0[ai] = xf;
+        geo->y0[ai] = yf;
+        geo->dx[ai] = dx;
+        geo->dy[ai] = dy;
+      }
+      auto rmin = [](int v) {
+        v = min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x111, 0xf, 0xf, false));
+        v = min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x112, 0xf, 0xf, false));
+        v = min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x114, 0xf, 0xf, false));
+        v = min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x118, 0xf, 0xf, false));
+        return __builtin_amdgcn_readlane(v, 15);
+      };
+      const int lo_x = rmin(act ? xf : 0x7fffffff), lo_y = rmin(act ? yf : 0x7fffffff);
+      const int hi_x = -rmin(act ? -xf : 0x7fffffff), hi_y = -rmin(act ? -yf : 0x7fffffff);
+      xlo = wave_uniform(max(lo_x - R, 0));
+      ylo = wave_uniform(max(lo_y - R, 0));
+      const int xhi = min(hi_x + R + 1, W2 - 1), yhi = min(hi_y + R + 1, H2 - 1);
+      bw = wave_uniform(xhi - xlo + 1);
+      bh = wave_uniform(yhi - ylo + 1);
+      if (bw <= 0 || bh <= 0 || !idx_ok) bw = bh = 0;
+      inner = bw > 0 && lo_x - R >= 0 && lo_y - R >= 0 && hi_x + R + 1 <= W2 - 1 &&
+              hi_y + R + 1 <= H2 - 1;
+      if constexpr (RAW9) {
+        const int kbv = (yf - R - ylo) * bw + (xf - R - xlo);
+        const float a00 = (1.f - dx) * (1.f - dy), a01 = dx * (1.f - dy), a10 = (1.f - dx) * dy,
+                    a11 = dx * dy;
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+          kb[k] = __builtin_amdgcn_readlane(kbv, k);
+          w00[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a00), k));
+          w01[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a01), k));
+          w10[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a10), k));
+          w11[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a11), k));
+        }
+      }
+    }
+    const int ntile = (bw * bh + 15) >> 4;
+    const bool fast = ntile <= kLvlMaxTiles;
+    float* dst = out + ((size_t)b * M + m) * nout * L + lev;
+
+    // bilinear + permute from G (correlation_kernel.cu:260-271), then this
+    // level's slice of the edge's [nout][L] block straight to HBM: output o
+    // of lane o % 64 (consecutive outputs in consecutive lanes, 16 B apart)
+    auto tap4 = [&](int k, int yy, int xx, bool mat, float& r00, float& r01, float& r10,
+                    float& r11) __attribute__((always_inline)) {
+      if (mat) {  // clamped (valid) LDS addresses, zeroed by a select
+        const int cap = max(bw * bh - 1, 0);
+        const int gy = geo->y0[k] + yy - R - ylo, gx = geo->x0[k] + xx - R - xlo;
+        const float* g = G + k * kLvlBoxStride;
+        const bool y0i = gy >= 0 && gy < bh, y1i = gy + 1 >= 0 && gy + 1 < bh;
+        const bool x0i = gx >= 0 && gx < bw, x1i = gx + 1 >= 0 && gx + 1 < bw;
+        const float a00 = g[min(max(gy * bw + gx, 0), cap)];
+        const float a01 = g[min(max(gy * bw + gx + 1, 0), cap)];
+        const float a10 = g[min(max((gy + 1) * bw + gx, 0), cap)];
+        const float a11 = g[min(max((gy + 1) * bw + gx + 1, 0), cap)];
+        r00 = (y0i && x0i) ? a00 : 0.f;
+        r01 = (y0i && x1i) ? a01 : 0.f;
+        r10 = (y1i && x0i) ? a10 : 0.f;
+        r11 = (y1i && x1i) ? a11 : 0.f;
+      } else {
+        const float* g = G + k * D * D;
+        r00 = g[yy * D + xx];
+        r01 = g[yy * D + xx + 1];
+        r10 = g[(yy + 1) * D + xx];
+        r11 = g[(yy + 1) * D + xx + 1];
+      }
+    };
+    auto bil = [&](int k, float r00, float r01, float r10, float r11) __attribute__((always_inline)) {
+      const float dx = geo->dx[k], dy = geo->dy[k];
+      float v = ((1.f - dx) * (1.f - dy)) * r00;
+      v = v + (dx * (1.f - dy)) * r01;
+      v = v + ((1.f - dx) * dy) * r10;
+      v = v + (dx * dy) * r11;
+      return v;
+    };
+    auto bilinear_store = [&](bool mat) __attribute__((always_inline)) {
+      if constexpr (RAW9) {
+        // lane = output point (xx = lane >> 3, yy = lane & 7), every k: uniform
+        // weights, no index division; through the stage into output order
+        const int xx = min(lane >> 3, Dp - 1), yy = min(lane & 7, Dp - 1);
+        const bool on = (lane >> 3) < Dp && (lane & 7) < Dp;
+        float v[9];
+        if (mat && inner) {  // every tap in the box: 4 reads at fixed offsets
+          const int loff = yy * bw + xx;
+#pragma unroll
+          for (int k = 0; k < 9; k++) {
+            const float* g = G + k * kLvlBoxStride + kb[k] + loff;
+            const float r00 = g[0], r01 = g[1], r10 = g[bw], r11 = g[bw + 1];
+            float t = w00[k] * r00;
+            t = t + w01[k] * r01;
+            t = t + w10[k] * r10;
+            t = t + w11[k] * r11;
+            v[k] = t;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 9; k++) {
+            float r00, r01, r10, r11;
+            tap4(k, yy, xx, mat, r00, r01, r10, r11);
+            v[k] = bil(k, r00, r01, r10, r11);
+          }
+        }
+        float* so = reinterpret_cast<float*>(stage);
+        if (on) {
+#pragma unroll
+          for (int k = 0; k < 9; k++) so[(xx * Dp + yy) * 9 + k] = v[k];
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int u = 0; u < 7; u++) {
+          const int o = lane + kWave * u;
+          const float vo = so[min(o, 440)];
+          if (o < 441) dst[(size_t)o * L] = vo;
+        }
+        wave_lds_sync();  // stage free again
+      } else {
+#pragma unroll
+        for (int u = 0; u < kOutPerLane; u++) {
+          const int o = lane + kWave * u;
+          const int k = min(o % np, np - 1), t = o / np, yy = min(t % Dp, Dp - 1),
+                    xx = min(t / Dp, Dp - 1);
+          float r00, r01, r10, r11;
+          tap4(k, yy, xx, mat, r00, r01, r10, r11);
+          const float v = bil(k, r00, r01, r10, r11);
+          if (o < nout) dst[(size_t)o * L] = v;
+        }
+      }
+    };
+    wave_lds_sync();  // geo visible
+    if (!fast) {
+      // windows too spread for the matrix path: raw[k][yy][xx] as fp32 dot
+      // products straight from HBM into G, then the bilinear
+      const float* f2 = static_cast<const float*>(LV_SEL(f2, lev)) +
+                        ((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 * C;
+      const float* f1 = fmap1 + ((size_t)b * N1 + (idx_ok ? ix : 0)) * C * np;
+      for (int e = lane; e < np * D * D; e += kWave) {
+        const int k = e / (D * D), t = e % (D * D), yy = t / D, xx = t % D;
+        const int i1 = geo->y0[k] + yy - R, j1 = geo->x0[k] + xx - R;
+        float sacc = 0.f;
+        if (idx_ok && i1 >= 0 && i1 < H2 && j1 >= 0 && j1 < W2) {
+          const float* px = f2 + ((size_t)i1 * W2 + j1) * C;
+          for (int c = 0; c < C; c++) sacc += f1[(size_t)c * np + k] * px[c];
+        }
+        G[e] = sacc;
+      }
+      wave_lds_sync();
+      bilinear_store(false);
+      wave_lds_sync();
+      return;
+    }
+
+    // box tiles as whole lines: instruction h of tile t covers pixels
+    // 16 t + 8 (h & 1) + (lane >> 3), 128-B quarter h >> 1, 16 B (lane & 7) each
+    const int npx = max(bw * bh, 1), bw1 = max(bw, 1);
+    const float* base = static_cast<const float*>(LV_SEL(f2, lev)) +
+                        (((size_t)b * N2 + (idx_ok ? jx : 0)) * H2 * W2 +
+                         (ntile > 0 ? (size_t)ylo * W2 + xlo : 0)) * C +
+                        4 * (lane & 7);
+    const int rowe = W2 * C;
+    const float rbw = 1.0f / (float)bw1;
+    const float* base0 = static_cast<const float*>(LV_SEL(f2, lev));
+    auto load_tile = [&](u32x4 (&d)[8], int t) __attribute__((always_inline)) {
+      // past the end (ring refills, never used): every lane reads the same 16 B,
+      // one line request per instruction instead of eight
+      const bool past = t >= ntile;
+      const float* s[2];
+#pragma unroll
+      for (int ph = 0; ph < 2; ph++) {
+        const int px = min(16 * t + 8 * ph + (lane >> 3), npx - 1);  // pad lanes: pixel npx - 1
+        const int r = (int)(((float)px + 0.5f) * rbw), cc = px - r * bw1;
+        s[ph] = past ? base0 : base + r * rowe + cc * C;
+      }
+#pragma unroll
+      for (int h = 0; h < 8; h++)
+        d[h] = *reinterpret_cast<const gu32x4*>(reinterpret_cast<uintptr_t>(s[h & 1] + 32 * (h >> 1)));
+    };
+    u32x4 ring[RING][8];
+    LVL_STAMP(1);
+    // unconditional preload (an empty box reads the frame's first pixel): the
+    // waits below then count exactly
+#pragma unroll
+    for (int k = 0; k < RING; k++) {
+      load_tile(ring[k], k);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    LVL_STAMP(2);
+
+    // A fragments: lane (i = lane & 15, q = lane >> 4) holds patch row i,
+    // channels 16 h + 4 q + s at a[4 h + s] (zero for rows i >= np)
+    float a[32];
+    {
+#pragma unroll
+      for (int r = 0; r < kPA; r++) reinterpret_cast<u32x4*>(G)[min(lane + kWave * r, n16 - 1)] = pa[r];
+      wave_lds_sync();
+      const bool arow = idx_ok && ai < np;
+      const int fi = min(ai, np - 1);
+#pragma unroll
+      for (int h = 0; h < 8; h++)
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+          const float v = G[(16 * h + 4 * aq + s) * np + fi];
+          a[4 * h + s] = arow ? v : 0.0f;
+        }
+      wave_lds_sync();  // G free again
+    }
+    LVL_STAMP(3);
+
+    // stage addresses: a lane writes its 16 B of pixel pt = 8 ph + (lane >> 3),
+    // chunk c = lane & 7 at pt * 128 + ((c ^ (pt & 7)) * 16); B fragment of
+    // lane (n, q), half j of the quarter: chunk 4 j + q of pixel n
+    const int wr0 = (lane >> 3) * 128 + (((lane & 7) ^ (lane >> 3)) << 4);
+    const int rd0 = ai * 128 + ((aq ^ (ai & 7)) << 4), rd1 = ai * 128 + (((4 + aq) ^ (ai & 7)) << 4);
+    auto step = [&](u32x4 (&cur)[8], int t) __attribute__((always_inline)) {
+      const bool live = t < ntile;
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      if (live) {
+#pragma unroll
+        for (int qt = 0; qt < 4; qt++) {
+          *reinterpret_cast<u32x4*>(stage + wr0) = cur[2 * qt];
+          *reinterpret_cast<u32x4*>(stage + 1024 + wr0) = cur[2 * qt + 1];
+          const float4 b0 = *reinterpret_cast<const float4*>(stage + rd0);
+          const float4 b1 = *reinterpret_cast<const float4*>(stage + rd1);
+          const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+          for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+              const float av = a[4 * (2 * qt + j) + s], bv = bb[4 * j + s];
+              if (s & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc1, 0, 0, 0);
+              else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc0, 0, 0, 0);
+            }
+        }
+      }
+      // refill this slot with tile t + RING (unconditional: every path into
+      // the next group has the same load order, the wait before a tile
+      // drains only that tile's loads)
+      load_tile(cur, t + RING);
+      if (live) {
+        // D: lane holds rows 4q + r (patch pixels), column lane & 15 (box pixel)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int row = 4 * aq + r;
+          if (row < np) G[row * kLvlBoxStride + 16 * t + ai] = acc0[r] + acc1[r];
+        }
+      }
+    };
+    for (int t = 0; t < ntile; t += RING) {
+#pragma unroll
+      for (int k = 0; k < RING; k++) {
+        step(ring[k], t + k);
+        if (t + k == 0) LVL_STAMP(4);
+      }
+    }
+    LVL_STAMP(5);
+    wave_lds_sync();
+    bilinear_store(true);
+    wave_lds_sync();  // G, stage and geo free for the next unit
+    LVL_STAMP(6);
+  };
+
+  if (w < L) {
+    const int pA = x8 * per + j8, pB = pA + half;
+    const int lim = order ? min(per * (x8 + 1), M) : nE;
+    if (pA < lim) run_unit(pA, w);
+    if (pB < lim && pB < x8 * per + per) run_unit(pB, L - 1 - w);
+  }
+}
+
 // [count, C, H, W] -> [count, H, W, C] (one 32 x 32 tile of (c, hw) per block)
 template <typename T>
 __global__ void __launch_bounds__(256)
@@ -749,6 +1137,14 @@ __global__ void __launch_bounds__(256)
 
 using namespace dpvo;
 
+// experiment switch (A/B of the per-edge and the per-level kernels)
+static int g_corr_variant = 1;
+DPVO_EXPORT int dpvo_corr_nhwc_variant(int v) {
+  const int old = g_corr_variant;
+  if (v >= 0) g_corr_variant = v;
+  return old;
+}
+
 DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
     const void* fmap1, const void* const* fmap2, const int* H2, const int* W2, const float* scale,
     int L, const float* coords, const int64_t* ii, const int64_t* jj, const int32_t* order, int B,
@@ -772,15 +1168,32 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   // D * D <= 256 > kBoxStride only for R > 5, which the fast path covers)
   const int D = 2 * radius + 2;
   if (D * D > kBoxStride) return DPVO_ERR_UNSUPPORTED;
+  const bool ordered = order && B == 1;
+  const int* ord = ordered ? (const int*)order : (const int*)nullptr;
+  hipStream_t st = as_stream(stream);
+  if (g_corr_variant != 0 && dtype == DPVO_F32) {
+    // one wave per (edge, level) unit, two units per wave, whole-line tiles
+    const size_t lsm = (size_t)L * corr_lvl_wave_bytes(np);
+    const unsigned per = ordered ? (unsigned)((M + 7) / 8) : (unsigned)(B * M);
+    const unsigned lg = ordered ? 8u * ((per + 1) / 2) : (per + 1) / 2;
+    const bool r9 = np == 9 && radius == 3;
+#define LVL_LAUNCH(RG, R9)                                                                       \
+  hipLaunchKernelGGL((corr_nhwc_lvl_kernel<RG, R9>), dim3(lg), dim3(L * kWave), lsm, st,         \
+                     (const float*)fmap1, lv, L, coords, ii, jj, B, M, np, N1, N2, radius, ord, out)
+    if (g_corr_variant == 3) {
+      if (r9) LVL_LAUNCH(3, true); else LVL_LAUNCH(3, false);
+    } else {
+      if (r9) LVL_LAUNCH(2, true); else LVL_LAUNCH(2, false);
+    }
+#undef LVL_LAUNCH
+    return launch_status();
+  }
   const size_t smem = corr_nhwc_lds_bytes(np, radius, L);
   const long long units = (long long)B * M;
   unsigned grid = (unsigned)((units + kNhwcWaves - 1) / kNhwcWaves);
-  const bool ordered = order && B == 1;
   if (ordered) grid = 8u * (unsigned)((grid + 7) / 8);
-  const int* ord = ordered ? (const int*)order : (const int*)nullptr;
   const bool raw9 = np == 9 && radius == 3;  // DPVO: p = 3, R = 3
   const dim3 g(grid), blk(kNhwcWaves * kWave);
-  hipStream_t st = as_stream(stream);
   if (dtype == DPVO_F16) {
     const __half* f1 = (const __half*)fmap1;
     if (raw9)

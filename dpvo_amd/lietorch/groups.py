@@ -257,42 +257,45 @@ class LieGroup:
 
 
 class LieGroupParameter(torch.Tensor):
-    """Tangent-space parameter of a group (groups.py:9-48)."""
+    """An optimisation variable on a group: a zero tangent vector (the leaf
+    tensor an optimiser sees and steps) anchored at ``group``.  Every group
+    operation acts on ``retr()`` = Exp(tangent) * anchor, and ``add_`` folds a
+    step into the anchor.  Public name and behaviour of lietorch's class
+    (dpvo/lietorch/groups.py:9-48); nothing on the update path uses it."""
 
-    from torch._C import _disabled_torch_function_impl
-
-    __torch_function__ = _disabled_torch_function_impl
+    __torch_function__ = torch._C._disabled_torch_function_impl
 
     def __new__(cls, group, requires_grad=True):
-        data = torch.zeros(group.tangent_shape, device=group.data.device, dtype=group.data.dtype,
-                           requires_grad=True)
-        return torch.Tensor._make_subclass(cls, data, requires_grad)
+        tangent = group.data.new_zeros(group.tangent_shape).as_subclass(cls)
+        tangent.requires_grad_(requires_grad)
+        tangent.group = group
+        return tangent
 
-    def __init__(self, group):
-        self.group = group
+    def __init__(self, group, requires_grad=True):  # state set in __new__
+        pass
 
     def retr(self):
         return self.group.retr(self)
 
-    def log(self):
-        return self.retr().log()
-
-    def inv(self):
-        return self.retr().inv()
-
-    def adj(self, a):
-        return self.retr().adj(a)
-
-    def __mul__(self, other):
-        if isinstance(other, LieGroupParameter):
-            return self.retr() * other.retr()
-        return self.retr() * other
-
     def add_(self, update, alpha):
         self.group = self.group.exp(alpha * update) * self.group
+        return self
 
-    def __getitem__(self, index):
-        return self.retr().__getitem__(index)
+    def __mul__(self, other):
+        rhs = other.retr() if isinstance(other, LieGroupParameter) else other
+        return self.retr() * rhs
+
+
+def _on_retraction(name):
+    def method(self, *args):
+        return getattr(self.retr(), name)(*args)
+
+    method.__name__ = name
+    return method
+
+
+for _name in ("log", "inv", "adj", "__getitem__"):
+    setattr(LieGroupParameter, _name, _on_retraction(_name))
 
 
 class SO3(LieGroup):

@@ -18,6 +18,9 @@
 #   stale      the stale-granule regression test; staledemo: its A/B on the round-4 tree
 #   corrmicro  A-CORR micro-bench (per-wave phase stamps) for each built variant
 #   launchprof rocprof kernel durations of the fused start-of-update launch and its parts
+#   corrvar    A-CORR kernel variants (scripts/corr_variants.py): time + deviation
+#   corrpmc    SQ / TCC counter passes over the corr variants (scripts/pmc_corrvar.sh)
+#   corrwide   the channels-last corr tests incl. the wide-dynamic-range ones
 #   cfg4       bench.py --sharded (cfg4 global BA, one rank)
 #   cfg4prof   rocprofv3 over the cfg4 bench
 #   pmcsq      BA/corr SQ + LDS counter passes (scripts/pmc.sh with PMC_GROUPS)
@@ -73,6 +76,9 @@ for s in "$@"; do
         -- python scripts/reproject_launch_bench.py cfg2 dpvo25
       python scripts/kstats.py "$(find $O/${T}_launchprof -name '*kernel_stats.csv' | head -1)" 12 \
         | tee $O/${T}_launchprof_kstats.txt ;;
+    corrvar) run corrvar 200 python -u scripts/corr_variants.py ${CORRVAR_ARGS:-} ;;
+    corrpmc) run corrpmc 700 bash scripts/pmc_corrvar.sh ;;
+    corrwide) run corrwide 300 $PYT tests/test_corr_gpu.py -k "wide_range or channels_last" ;;
     cfg4) run cfg4 300 python -u bench.py --sharded --steps 5 --warmup 2 ;;
     cfg4prof) prof cfg4prof --sharded --steps 3 --warmup 1 ;;
     pmcsq) run pmcsq 600 env PMC_GROUPS="${PMC_GROUPS:-SQ_WAIT_ANY SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES}" bash scripts/pmc.sh ;;

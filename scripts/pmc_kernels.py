@@ -13,7 +13,12 @@ SHORT = [("corr_nhwc", "corr"), ("ba_window_kernel", "ba_window"),
          ("corr_nchw", "corr_nchw")]
 
 
+FULL = False  # argv[2] == "full": group by the whole kernel name (template variants apart)
+
+
 def short(name):
+    if FULL:
+        return name.split("(")[0][-70:] if any(k in name for k, _ in SHORT) else None
     for k, v in SHORT:
         if k in name:
             return v
@@ -21,6 +26,8 @@ def short(name):
 
 
 def main():
+    global FULL
+    FULL = len(sys.argv) > 2 and sys.argv[2] == "full"
     for f in sorted(glob.glob(sys.argv[1] if len(sys.argv) > 1 else
                               "gpurun_out/pmc_*/run_counter_collection.csv")):
         per = collections.defaultdict(float)

@@ -525,3 +525,55 @@ def test_nchw_fp32_cfg2_matches_channels_last(cc, gpu):
                               (coords / s).cpu().numpy()[:, sel], kk1.cpu().numpy()[sel],
                               jj1.cpu().numpy()[sel], 3)
         _close(a.cpu().numpy()[:, sel], ref)
+
+
+# ---- fp32 features over a wide dynamic range: the
+# channels-last fp32 path must hold the fp32 bar whatever the magnitudes
+def _wide(seed, kind):
+    f1, f2, co, ii, jj, R = _case(seed, M=96, C=128, H2=40, W2=48)
+    r = np.random.default_rng(seed + 7)
+    if kind == "channel_scales":  # per-channel scales 1e-4 .. 1e3 on both sides
+        f1 = f1 * 10.0 ** r.uniform(-4, 3, (1, 1, 128, 1, 1))
+        f2 = f2 * 10.0 ** r.uniform(-4, 3, (1, 1, 128, 1, 1))
+    elif kind == "tiny":  # every feature ~1e-4 (f16-subnormal territory)
+        f1, f2 = f1 * 1e-4, f2 * 1e-4
+    elif kind == "large_a_tiny_b":
+        f1, f2 = f1 * 1e3, f2 * 1e-4
+    elif kind == "f16_edges":  # magnitudes at 2^-24, 2^-14, 2^-3, 1, 16
+        e = r.choice([-24, -14, -3, 0, 4], size=f2.shape)
+        f2 = np.sign(f2) * 2.0 ** e * (1 + 0.01 * r.standard_normal(f2.shape))
+        e1 = r.choice([-14, -3, 0], size=f1.shape)
+        f1 = np.sign(f1) * 2.0 ** e1 * (1 + 0.01 * r.standard_normal(f1.shape))
+    elif kind == "beyond_f16":  # |b| >= 65520 in some pixels of the fine level
+        m = r.random(f2.shape) < 0.02
+        f2 = np.where(m, np.sign(f2) * r.uniform(65520, 3e5, f2.shape), f2)
+    return f1.astype(np.float32), f2.astype(np.float32), co, ii, jj, R
+
+
+@pytest.mark.parametrize("kind", ["channel_scales", "tiny", "large_a_tiny_b", "f16_edges",
+                                  "beyond_f16"])
+def test_channels_last_fp32_wide_range(gpu, kind):
+    """Element-wise against the fp64 oracle: relative error <= 1e-4 wherever
+    |ref| >= 1e-3 max|ref|, and everywhere |err| <= 1e-4 |ref| + 2^-20 S with
+    S = the same correlation of |f1|, |f2| (the magnitude of the summed
+    products: the fp32 summation-noise scale).  A plain sequential fp32 dot
+    (the CUDA kernel's loop) measures 2.7e-5 .. 5.5e-5 on these cases under
+    the first bar and needs 1.4e-8 .. 1.1e-7 S under the second."""
+    from dpvo_amd import altcorr, synthetic
+
+    f1, f2, co, ii, jj, R = _wide(41, kind)
+    levels = (1, 4)
+    lv1 = _t(f2, gpu)
+    pyr = [lv1, torch.nn.functional.avg_pool2d(lv1[0], 4, 4).unsqueeze(0)]
+    out = altcorr.corr_levels(_t(f1, gpu), [synthetic.channels_last(p) for p in pyr],
+                              _t(co, gpu), _t(ii, gpu), _t(jj, gpu), R, scales=levels)
+    out = out.view(1, len(ii), 2 * R + 1, 2 * R + 1, 3, 3, len(levels)).double().cpu().numpy()
+    for l, s in enumerate(levels):
+        p = pyr[l].cpu().numpy()
+        ref = oracle.corr_fwd(f1, p, co / s, ii, jj, R).astype(np.float64)
+        mag = oracle.corr_fwd(np.abs(f1), np.abs(p), co / s, ii, jj, R).astype(np.float64)
+        err = np.abs(out[..., l] - ref)
+        big = np.abs(ref) >= 1e-3 * np.abs(ref).max()
+        rel = (err[big] / np.abs(ref[big])).max()
+        assert rel <= 1e-4, (kind, s, rel)
+        assert (err <= 1e-4 * np.abs(ref) + 2.0 ** -20 * mag).all(), (kind, s)

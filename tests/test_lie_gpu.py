@@ -134,3 +134,24 @@ def test_se3_retr_matches_fastba_retraction(gpu):
     Y = X.retr(a)
     Z = SE3.exp(a) * X
     assert torch.allclose(Y.data, Z.data, atol=1e-12)
+
+
+def test_lie_group_parameter(gpu):
+    """LieGroupParameter: zero tangent leaf anchored at the group; retr() is
+    the anchor, gradients reach the tangent, add_ moves the anchor."""
+    from dpvo_amd.lietorch import SE3, LieGroupParameter
+
+    torch.manual_seed(0)
+    g = SE3.exp(0.3 * torch.randn(5, 6, device=gpu, dtype=torch.float64))
+    p = LieGroupParameter(g)
+    assert p.shape == (5, 6) and p.requires_grad and p.is_leaf
+    assert torch.allclose(p.retr().data, g.data, atol=1e-12)
+    assert torch.allclose(p.log(), g.log(), atol=1e-12)
+    assert torch.allclose(p.inv().data, g.inv().data, atol=1e-12)
+    (p.retr().log() ** 2).sum().backward()
+    assert p.grad is not None and torch.isfinite(p.grad).all() and p.grad.abs().sum() > 0
+    step = 0.1 * torch.randn(5, 6, device=gpu, dtype=torch.float64)
+    p.add_(step, 0.5)
+    assert torch.allclose(p.group.data, (SE3.exp(0.5 * step) * g).data, atol=1e-12)
+    q = LieGroupParameter(g)
+    assert torch.allclose((p * q).data, (p.group * g).data, atol=1e-12)
