@@ -38,7 +38,7 @@ sys.path.insert(0, REPO)
 METRIC = "update-iterations/sec (altcorr+fastba) on 96-patch/2048-edge graph, 1→8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                            "profiles", "r05_corr_traffic.json")
+                            "profiles", "r06_corr_traffic.json")
 
 
 def pmc_traffic(config):
@@ -545,12 +545,12 @@ def main():
                 "parallelism": f"replicas x{world}",
             },
             "roofline": {
-                "kernel": "corr_nhwc_kernel (A-CORR, all levels, one launch)",
+                "kernel": ("corr_nhwc_lvl_kernel (A-CORR, all levels, one launch, one wave per "
+                           "(edge, level))" if args.features == "f32" else
+                           "corr_nhwc_kernel (A-CORR, all levels, one launch)"),
                 # how the fp32 products are formed
-                "products": ("fp32 features: a*b = ah*bh + ah*bl + (al*bh)*2^-11 from f16 "
-                             "pieces on v_mfma_f32_16x16x32_f16, fp32 accumulation "
-                             "(per-product error <= ~2^-21|a||b| + 2^-25|a|); "
-                             "non-finite levels redone in plain fp32"
+                "products": ("fp32 x fp32 on v_mfma_f32_16x16x4_f32 (IEEE fp32 products), fp32 "
+                             "accumulation"
                              if args.features == "f32" else
                              "fp16 x fp16 on v_mfma_f32_16x16x32_f16, fp32 accumulation"),
                 "bound": "hbm",
@@ -563,6 +563,10 @@ def main():
                 # live kernel time; below `achieved` because edges sharing a
                 # target frame re-read overlapping boxes from L2 / MALL
                 "traffic_gbs": (traffic / (corr_ms * 1e-3) / 1e9) if traffic else None,
+                # the same as a fraction of the peak: `frac` counts every byte the
+                # kernel's loads request (the survey's per-edge count), re-reads
+                # served by L2 / MALL included, so it can exceed 1
+                "traffic_frac": (traffic / (corr_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "kernel_ms": corr_ms,
                 "per_level": per_level,

@@ -5,10 +5,6 @@
 
 #include "common.hpp"
 
-// per-phase shader-clock stamps (micro-benchmark builds only)
-#ifndef BGJ_STAMP
-#define BGJ_STAMP(k)
-#endif
 
 namespace dpvo {
 namespace gba {
@@ -35,10 +31,8 @@ __device__ __forceinline__ double rcp_f64(double p) {
 // entry per lane, pivot row / column by shuffles); (2b) every thread forms one
 // entry of W = P^-1 Rw and of V = Cw P^-1; (3) every entry outside the block
 // gets a -= Cw_i . W_j (6 FMAs), block rows W, block columns -V, the pivot P^-1.
-// BGJ_THREAD_PIVOT (experiment): (2a) + (2b) replaced by right-hand-side
-// solves from a per-thread Cholesky of P, one barrier less -- measured equal
-// (78.0k vs 79.0k cycles at m = 72: the per-thread fp64 sqrt / reciprocal
-// chain costs what the barrier and the wave-0 chain did).
+// (A per-thread Cholesky of P instead of (2a) + (2b), one barrier less,
+// measured equal: 78.0k vs 79.0k cycles at m = 72; DESIGN.md.)
 // W, V, P^-1 are single-buffered: their writers of step K + 1 have passed
 // barrier (1) of K + 1, so every reader of step K is done.
 // vbuf: 2 (Rw + Cw) + W + V + P^-1 = 2 * 12 kMaxM + 12 kMaxM + 36 doubles.
@@ -60,7 +54,6 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
   double* V = W + 6 * kMaxM;      // [kMaxM][6]
   double* Pi = V + 6 * kMaxM;     // [36]
   const int nb = n / 6;
-  BGJ_STAMP(0);
   for (int K = 0; K < nb; K++) {
     const int b0 = 6 * K;
     double* Rw = vbuf + (K & 1) * 12 * kMaxM;  // [6][kMaxM]
@@ -86,8 +79,7 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
       }
     }
     __syncthreads();
-    BGJ_STAMP(1 + 4 * K);
-#ifndef BGJ_THREAD_PIVOT  // wave 0 inverts P, then W and V by products
+    // wave 0 inverts P, then W and V by products
     // (2a) wave 0: P^-1
     if (tid < kWave) {
       // lane 6 r + c holds P[r][c]; pivot row / column by lane shuffles
@@ -110,7 +102,6 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
       if (tid < 36) Pi[tid] = x;
     }
     __syncthreads();
-    BGJ_STAMP(2 + 4 * K);
     // (2b) W = P^-1 Rw and V = Cw P^-1, one entry of each per thread
     for (int q = tid; q < 6 * n; q += blockDim.x) {
       const int d = q / n, j = q - d * n;  // W[d][j]
@@ -125,74 +116,6 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
       V[i * 6 + e] = sv;
     }
     __syncthreads();
-    BGJ_STAMP(3 + 4 * K);
-#else
-    // (2) W = P^-1 Rw, V = Cw P^-1 (= (P^-1 Cw^T)^T, P symmetric) and P^-1 by
-    // right-hand sides: n columns of Rw, n rows of Cw, 6 unit vectors, one per
-    // thread, each thread factoring P = L L^T itself in registers (P is an SPD
-    // Schur complement).  No wave-0 pivot chain and one barrier per block step
-    // less than inverting P first (profiles/r04_cfg4_bgj_phases.txt).
-    for (int q = tid; q < 2 * n + 6; q += blockDim.x) {
-      double l[21];  // lower triangle, packed by rows: l[i (i + 1) / 2 + j]
-#pragma unroll
-      for (int i = 0; i < 6; i++)
-#pragma unroll
-        for (int j = 0; j <= i; j++) l[i * (i + 1) / 2 + j] = Rw[i * kMaxM + b0 + j];
-      double x[6];
-#pragma unroll
-      for (int u = 0; u < 6; u++) {  // unconditional reads, then select
-        const double r = Rw[u * kMaxM + min(q, n - 1)];
-        const double c = Cw[min(max(q - n, 0), n - 1) * 6 + u];
-        x[u] = q < n ? r : (q < 2 * n ? c : (u == q - 2 * n ? 1.0 : 0.0));
-      }
-      bool ok = true;
-      double rd[6];
-#pragma unroll
-      for (int j = 0; j < 6; j++) {
-        double d = l[j * (j + 1) / 2 + j];
-#pragma unroll
-        for (int k = 0; k < j; k++) d = fma(-l[j * (j + 1) / 2 + k], l[j * (j + 1) / 2 + k], d);
-        ok = ok && d > 0.0;
-        const double sd = sqrt(d > 0.0 ? d : 1.0);
-        rd[j] = rcp_f64(sd);
-#pragma unroll
-        for (int i = j + 1; i < 6; i++) {
-          double v = l[i * (i + 1) / 2 + j];
-#pragma unroll
-          for (int k = 0; k < j; k++) v = fma(-l[i * (i + 1) / 2 + k], l[j * (j + 1) / 2 + k], v);
-          l[i * (i + 1) / 2 + j] = v * rd[j];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 6; i++) {  // L z = x
-        double v = x[i];
-#pragma unroll
-        for (int k = 0; k < i; k++) v = fma(-l[i * (i + 1) / 2 + k], x[k], v);
-        x[i] = v * rd[i];
-      }
-#pragma unroll
-      for (int i = 5; i >= 0; i--) {  // L^T w = z
-        double v = x[i];
-#pragma unroll
-        for (int k = i + 1; k < 6; k++) v = fma(-l[k * (k + 1) / 2 + i], x[k], v);
-        x[i] = v * rd[i];
-      }
-      if (!ok) bad = 1;
-      if (q < n) {
-#pragma unroll
-        for (int u = 0; u < 6; u++) W[u * kMaxM + q] = x[u];
-      } else if (q < 2 * n) {
-#pragma unroll
-        for (int u = 0; u < 6; u++) V[(q - n) * 6 + u] = x[u];
-      } else {
-#pragma unroll
-        for (int u = 0; u < 6; u++) Pi[u * 6 + (q - 2 * n)] = x[u];
-      }
-    }
-    __syncthreads();
-    BGJ_STAMP(2 + 4 * K);
-    BGJ_STAMP(3 + 4 * K);
-#endif
     // (3) update, branch-free except for the few waves holding block rows
     // (padding entries i, j >= n are computed from clamped rows and never
     // published or stored)
@@ -241,7 +164,6 @@ __device__ __forceinline__ bool wg_bgj_inverse(const double* src, int n, int lda
           if (p == ps) a[p][q] = v;
       }
     }
-    BGJ_STAMP(4 + 4 * K);
   }
   __syncthreads();
 #pragma unroll

@@ -200,18 +200,6 @@ __device__ __forceinline__ void residual64(const double* S, const double* y, con
   if (row < n && part == 0) v[row] = (float)(y[row] - s);
 }
 
-#ifdef WSOLVE_STEP_STAMPS
-#define WSTAMP_DBG(slot)                                                        \
-  do {                                                                          \
-    __builtin_amdgcn_sched_barrier(0);                                          \
-    if (st && k == 2 && lane == 0) st[slot] = (long long)__builtin_amdgcn_s_memtime(); \
-    __builtin_amdgcn_sched_barrier(0);                                          \
-  } while (0)
-#else
-#define WSTAMP_DBG(slot) \
-  do {                   \
-  } while (0)
-#endif
 __device__ __forceinline__ void wstamp(long long* st, int slot) {
   if (st && threadIdx.x == 0) st[slot] = (long long)__builtin_amdgcn_s_memtime();
 }
@@ -464,7 +452,6 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
 #pragma unroll
           for (int z = 0; z < 6; z++) v1[z] -= dot6(a, B + 6 * z);
         }
-        WSTAMP_DBG(56);
         float m[6][6], L[6][6], ri[6];
         // the 21 lower pivot entries (row r = lane r's v0) to every lane by
         // v_readlane: 33.1k vs 34.9k cycles per N = 11 solve against a store
@@ -475,9 +462,7 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
 #pragma unroll
           for (int c = 0; c <= r; c++)
             m[r][c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v0[c]), r));
-        WSTAMP_DBG(57);
         const bool ok = chol6_m(m, L, ri);
-        WSTAMP_DBG(58);
         if (!ok && lane == 0) *fail = 1;
         {
           // ONE forward substitution per lane: lanes 0-5 solve for unit vectors
@@ -497,7 +482,6 @@ __device__ inline bool wsolve(const WSolve& s, int N, int refine, int* fail,
             st_row(s.A + 36 * lblk(ia, c1) + 6 * xa, z);
           }
         }
-        WSTAMP_DBG(59);
         if (lane + 64 < nr) {
           float lv[6];
           fwd6(L, ri, v1, lv);

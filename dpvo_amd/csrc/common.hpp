@@ -12,6 +12,7 @@
 namespace dpvo {
 
 constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+constexpr int kMaxDevices = 64;  // per-device one-time host state (function attributes)
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -486,15 +486,20 @@ template <typename T>
 int nc_launch(const void* fmap1, const NcLevels& lv, bool use_scale, const float* coords,
               const int64_t* ii, const int64_t* jj, int B, int M, int np, int N1, int N2, int R,
               int L, int ordered, void* out_t, float* out_f, hipStream_t s) {
-  static bool attr = false;  // 4 x 17.7 KB per workgroup (+ the order's 4 edge ids): above 64 KB
-  if (!attr) {
+  // 4 x 17.7 KB per workgroup (+ the order's 4 edge ids): above 64 KB, set
+  // once per device; if the attribute cannot be set the caller's VALU kernel
+  // runs instead (DPVO_ERR_UNSUPPORTED)
+  static bool attr[kMaxDevices] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return DPVO_ERR_UNSUPPORTED;
+  if (!attr[dev]) {
     if (hipFuncSetAttribute((const void*)corr_nchw_kernel<T>,
                             hipFuncAttributeMaxDynamicSharedMemorySize,
                             kNcWaves * kNcWaveBytes + 16) != hipSuccess) {
       (void)hipGetLastError();  // not sticky: report it here, not at a later launch
-      return DPVO_ERR_LAUNCH;
+      return DPVO_ERR_UNSUPPORTED;
     }
-    attr = true;
+    attr[dev] = true;
   }
   unsigned gx = (unsigned)(((long long)B * M + kNcWaves - 1) / kNcWaves);
   if (ordered) gx = 8u * ((gx + 7u) / 8u);

@@ -288,6 +288,10 @@ torch::Tensor ba_forward_marks(torch::Tensor poses, torch::Tensor patches,
 
 // The marks a workspace holds (after launches made with set_marks(true)).
 torch::Tensor ba_workspace_marks(torch::Tensor ws, int64_t E, int t0, int t1) {
+  check_device(ws, "ws");
+  TORCH_CHECK(E >= 0 && t1 > t0, "cuda_ba.workspace_marks: bad E / window");
+  TORCH_CHECK((size_t)ws.nbytes() >= dpvo_ba_workspace_bytes((int)E, t0, t1),
+              "cuda_ba.workspace_marks: ws is not a BA workspace planned for (E, t0, t1)");
   auto out = torch::zeros({2432}, ws.options().dtype(torch::kInt64));
   check_status(dpvo_ba_phase_marks(ws.data_ptr(), (int)E, t0, t1, out.data_ptr<int64_t>(),
                                    current_stream()),

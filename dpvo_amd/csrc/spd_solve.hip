@@ -2,10 +2,11 @@
 // surface's CholeskySolver (dpvo/ba.py:13-38: torch.linalg.cholesky_ex +
 // cholesky_solve; block_solve 67-77 feeds it the damped pose system).
 //
-// One 256-thread workgroup per batch item.  The matrix lives in LDS when it
-// fits (fp64 n <= 120, fp32 n <= 170: every DPVO training / python_ba
-// system), else in the caller's factor buffer in HBM (same code, global
-// addresses); the work is latency-bound either way (n column steps).
+// One 256-thread workgroup per batch item.  The matrix and the right-hand
+// sides live in LDS when n (n + k) elements fit 160 KB - 64 B (one rhs: fp64
+// n <= 142, fp32 n <= 201; every DPVO training / python_ba system), else in
+// the caller's factor buffer in HBM (same code, global addresses); the work
+// is latency-bound either way (n column steps).
 //   factor: right-looking Cholesky on the lower triangle (torch reads only
 //           the lower triangle of H, cholesky_ex default upper=False):
 //           column j: pivot d = a_jj (d <= 0 or NaN: info = j + 1, the
@@ -130,11 +131,18 @@ int spd_launch(const void* H, const void* B, void* L, void* X, int32_t* info, in
   const int in_lds = lds <= kSpdLds - 64;
   if (!in_lds && factor && !L) return DPVO_ERR_INVALID;  // the HBM working copy is the factor buffer
   if (in_lds && lds > 64 * 1024) {
-    // the dynamic LDS beyond the default 64 KB (the static fail flag sits on top)
-    if (hipFuncSetAttribute((const void*)spd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(kSpdLds - 64)) != hipSuccess) {
-      (void)hipGetLastError();  // not sticky: the launch reports its own status
-      return DPVO_ERR_LAUNCH;
+    // the dynamic LDS beyond the default 64 KB (the static fail flag sits on
+    // top), set once per device and instantiation
+    static bool attr_set[kMaxDevices] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return DPVO_ERR_LAUNCH;
+    if (!attr_set[dev]) {
+      if (hipFuncSetAttribute((const void*)spd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(kSpdLds - 64)) != hipSuccess) {
+        (void)hipGetLastError();  // not sticky: the launch reports its own status
+        return DPVO_ERR_LAUNCH;
+      }
+      attr_set[dev] = true;
     }
   }
   hipLaunchKernelGGL(spd_kernel<T>, dim3(batch), dim3(kSpdThreads), in_lds ? lds : 0,

@@ -15,7 +15,7 @@ import json
 import statistics
 import sys
 
-KERNEL = "corr_nhwc_kernel"
+KERNEL = "corr_nhwc_lvl_kernel"  # the fp32 A-CORR kernel of the bench (round 6)
 
 
 def per_launch(counter):

@@ -28,7 +28,9 @@ def test_forward_matches_direct_solve(gpu):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,k,dtype,tol", [(6, 1, torch.float64, 1e-10), (66, 3, torch.float64, 1e-10),
                                            (150, 2, torch.float64, 1e-9),  # HBM working copy
-                                           (66, 1, torch.float32, 2e-4), (200, 1, torch.float32, 5e-4)])
+                                           (66, 1, torch.float32, 2e-4), (200, 1, torch.float32, 5e-4),
+                                           (210, 1, torch.float32, 5e-4),  # fp32 HBM working copy
+                                           (120, 300, torch.float32, 5e-4)])  # k pushes it out of LDS
 def test_spd_solve_matches_dense(gpu, n, k, dtype, tol):
     from dpvo_amd.ba import _cuda_ba
 
