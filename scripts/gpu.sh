@@ -81,7 +81,7 @@ for s in "$@"; do
     corrwide) run corrwide 300 $PYT tests/test_corr_gpu.py -k "wide_range or channels_last" ;;
     cfg4) run cfg4 300 python -u bench.py --sharded --steps 5 --warmup 2 ;;
     cfg4prof) prof cfg4prof --sharded --steps 3 --warmup 1 ;;
-    pmcsq) run pmcsq 600 env PMC_GROUPS="${PMC_GROUPS:-SQ_WAIT_ANY SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES}" bash scripts/pmc.sh ;;
+    pmcsq) run pmcsq 600 env SQ_EXTRA="${SQ_EXTRA:-SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE}" bash scripts/pmc_sq.sh ;;
     traffic) run traffic 400 env PMC_GROUPS="FETCH_SIZE WRITE_SIZE" bash scripts/pmc.sh ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

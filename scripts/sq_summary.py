@@ -12,7 +12,7 @@ acc = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(f"{root}/sq_*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
-        short = next((k for k in ("ba_window_kernel", "ba_plan_kernel", "corr_nhwc_kernel", "reproject_plan_insert_kernel",
+        short = next((k for k in ("ba_window_kernel", "ba_plan_kernel", "corr_nhwc_lvl_kernel", "corr_nhwc_kernel", "reproject_plan_insert_kernel",
                                   "pyramid_insert_kernel", "reproject_kernel") if k in name), None)
         if short is None:
             continue
