@@ -10,29 +10,19 @@
 // every fmap2 load touches a partial 128-B line; channels-last makes each
 // window row one contiguous run of (width x C x 4) bytes.  The per-edge GEMM
 //     G[k][px] = sum_c f1[c][k] * f2[px][c]     (k < p*p, px in the union
-// bounding box of the edge's windows) runs on the matrix cores:
-// v_mfma_f32_16x16x4_f32 with A = f1 (16 rows >= p*p, loaded once per edge
-// and shared by every level), B = 16 box pixels x 4 channels straight from
-// HBM as one 16-B load per lane (a lane's float4 holds 4 channels = 4
-// consecutive K steps), D = G tile -> LDS.  One wave per edge handles every
-// level; the bilinear + permute of all levels is kept in registers and
-// stored once per edge as contiguous [.., L] float4 rows.
+// bounding box of the edge's windows) runs on the matrix cores, then the
+// bilinear + permute reads the windows out of G.  Two kernels:
+//   corr_nhwc_lvl_kernel  fp32 features: one wave per (edge, level) unit,
+//                         whole-line tile loads through an LDS stage, exact
+//                         fp32 products (v_mfma_f32_16x16x4_f32);
+//   corr_nhwc_kernel      fp16 features (the fork's MIXED_PRECISION rings):
+//                         one wave per edge over every level,
+//                         v_mfma_f32_16x16x32_f16 with fp32 accumulation.
 #include <type_traits>
 
 #include "common.hpp"
 #include "pyr_insert.hpp"
 
-// diagnostic builds (scripts/micro/corr_bench.hip) define CORR_STAMP(slot) to
-// record per-wave shader-clock stamps; the library compiles it away
-#ifndef CORR_TSTAMP  // per-tile stamps (diagnostic builds): tile i, point k
-#define CORR_TSTAMP(i, k)
-#define CORR_TSTAMP_INIT
-#endif
-#ifndef CORR_STAMP
-#define CORR_STAMP(slot)
-#define CORR_STAMP_RT(slot)
-#define CORR_STAMP_ID(slot)
-#endif
 
 namespace dpvo {
 
@@ -84,7 +74,7 @@ struct alignas(16) TileDesc {
 inline size_t corr_nhwc_lds_bytes(int np, int R, int L) {
   return sizeof(float) * kNhwcWaves * np * kBoxStride + sizeof(NhwcGeom) * kNhwcWaves * kMaxL +
          sizeof(float) * kNhwcWaves * corr_obuf_floats(np, R, L) +
-         sizeof(TileDesc) * kNhwcWaves * kMaxL + 16 * 4 * kWave * kNhwcWaves;
+         sizeof(TileDesc) * kNhwcWaves * kMaxL;
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -136,8 +126,8 @@ __device__ __forceinline__ f16x4 h4_hi(u32x4 v) {
   return __builtin_bit_cast(f16x4, (u32x2){v.z, v.w});
 }
 
-// One wave per edge, every level (the gmap patch and the coordinates are
-// loaded once per edge).  The kernel is latency-bound: at DPVO sizes there
+// fp16 features: one wave per edge, every level (the gmap patch and the
+// coordinates are loaded once per edge).  The kernel is latency-bound: at DPVO sizes there
 // are only 8 edges per CU, so the bytes each wave keeps in flight decide the
 // bandwidth.  Design:
 //  * the gmap patch arrives with 16-B coalesced loads, staged through LDS;
@@ -187,10 +177,6 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     if (edge >= B * M) return;  // waves are independent: no block barrier below
   }
   const int b = edge / M, m = edge % M;
-  CORR_TSTAMP_INIT;
-  CORR_STAMP(0);
-  CORR_STAMP_RT(12);
-  CORR_STAMP_ID(14);
   const int ix = wave_uniform((int)ii[m]), jx = wave_uniform((int)jj[m]);
   const bool idx_ok = ix >= 0 && ix < N1 && jx >= 0 && jx < N2;
   const int C = kNhwcC, D = 2 * R + 2, Dp = D - 1, nout = Dp * Dp * np;
@@ -201,17 +187,10 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   // fragments: lane (i = lane & 15, q = lane >> 4) holds f1[c][i] for
   // c = 16h + 4q + s at K step 4h + s (the same channel order as the B loads)
   const int ai = lane & 15, aq = lane >> 4;
-  constexpr bool kHalf = std::is_same<T, __half>::value;
-  // fp32 features: split-f16 A fragments (see mma below).  K step t of a
-  // v_mfma_f32_16x16x32_f16 takes, for lane (i, q), the 8 channels
-  // 16 (2t) + 4q + {0..3} and 16 (2t + 1) + 4q + {0..3} of patch pixel i --
-  // the channels of the lane's B loads B[2t], B[2t + 1] of a tile.
-  //   a = (Ah + Al 2^-11) 2^ae     (ae != 0 only if the patch holds |a| >= 2^14)
-  f16x8 Ah[kHalf ? 1 : 4];
-  // the al' fragments [t][lane] in LDS (read once per K step of a tile)
-  f16x8* Alds = reinterpret_cast<f16x8*>(td + kNhwcWaves * kMaxL - wid * kMaxL) + wid * 4 * kWave;
-  float ainv = 1.0f;  // 2^ae: multiplies the tile sums
-  f16x4 Afh[kHalf ? kNhwcC / 16 : 1];
+  static_assert(std::is_same<T, __half>::value,
+                "fp16 features only: fp32 runs corr_nhwc_lvl_kernel (exact fp32 products)");
+  constexpr bool kHalf = true;
+  f16x4 Afh[kNhwcC / 16];
   // the patch's loads are issued here; they are staged into the A fragments
   // only after the first box tiles have been issued (build_A below), so the
   // gmap round trip and the first tiles' round trip overlap
@@ -244,33 +223,6 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
         for (int s = 0; s < 4; s++) {
           Afh[h][s] = arow ? (_Float16)__half2float(Gh[(32 * aq + 4 * h + s) * np + ai])
                            : (_Float16)0.0f;
-        }
-    } else {
-      float a[kNhwcC / 4];  // a[8t + j]: K step t, element j (channel 16 (2t + j/4) + 4q + j%4)
-#pragma unroll
-      for (int h = 0; h < kNhwcC / 16; h++)
-#pragma unroll
-        for (int s = 0; s < 4; s++) a[4 * h + s] = arow ? G[(16 * h + 4 * aq + s) * np + ai] : 0.0f;
-      // patch magnitude (wave max of |a| as bits: non-negative floats order
-      // like ints): a patch with |a| >= 2^14 is scaled by an exact power of
-      // two so its f16 pieces cannot overflow; the tile sums are scaled back
-      int mb = 0;
-#pragma unroll
-      for (int k = 0; k < kNhwcC / 4; k++) mb = max(mb, (int)(__float_as_uint(a[k]) & 0x7fffffffu));
-      mb = wave_max_i(mb);
-      const int ae = (mb >= 0x46800000 && mb < 0x7f800000) ? ((mb >> 23) - 127) - 13 : 0;
-      const float asc = __uint_as_float((unsigned)(127 - ae) << 23);
-      ainv = __uint_as_float((unsigned)(127 + ae) << 23);
-      f16x8 al;
-#pragma unroll
-      for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const float v = a[8 * t + j] * asc;
-          const _Float16 hv = (_Float16)v;
-          Ah[t][j] = hv;
-          al[j] = (_Float16)((v - (float)hv) * 2048.0f);
-          if (j == 7) Alds[t * kWave + lane] = al;
         }
     }
     wave_lds_sync();  // A fragments read: G free again
@@ -326,11 +278,7 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   // SIMD (hardware wave slot, HW_ID[3:0]) walks the levels coarse -> fine, so
   // the two waves of a SIMD are in opposite phases instead of both waiting on
   // memory first and both multiplying later.
-#ifdef CORR_NO_REV  // diagnostic builds (scripts/micro/corr_bench): every wave fine -> coarse
-  const bool rev = false;
-#else
   const bool rev = (__builtin_amdgcn_s_getreg((3 << 11) | 4) & 1) != 0;
-#endif
   auto level_at = [&](int j) { return rev ? L - 1 - j : j; };  // position -> level
   cum[0] = 0;
 #pragma unroll
@@ -338,7 +286,6 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
     const int nt = (j < L) ? wave_uniform(geo[level_at(j)].ntile) : 0;
     cum[j + 1] = cum[j] + ((nt <= kMaxTiles) ? nt : 0);
   }
-  CORR_STAMP(1);
 
   // ---- outputs.  Generic: lane owns outputs o = lane + 64u, decoded once
   // into (k, yy, xx).  RAW9: lane = (rx, ry) = (lane >> 3, lane & 7) owns the
@@ -500,15 +447,8 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
       const T* s = static_cast<const T*>(d.base) + pix(ai) + CorrT<T>::kLaneCh * aq;
 #pragma unroll
       for (int h = 0; h < V; h++)
-#if defined(CORR_DIAG_NO_LOAD)  // diagnostic builds only: no tile loads
-        dst[h] = (u32x4){(unsigned)h, (unsigned)i, 0u, 0u};
-#elif defined(CORR_NT_LOADS)  // diagnostic builds: streaming (non-temporal) tile loads
-        dst[h] = __builtin_nontemporal_load(reinterpret_cast<const gu32x4*>(
-            reinterpret_cast<uintptr_t>(s + (kHalf ? 8 * h : 16 * h))));
-#else
         dst[h] = *reinterpret_cast<const gu32x4*>(
             reinterpret_cast<uintptr_t>(s + (kHalf ? 8 * h : 16 * h)));
-#endif
     }
   };
   u32x4 ring[kRing][V];
@@ -528,9 +468,8 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   }
   build_A();
   // Level l the scalar way: raw[k][yy][xx] as fp32 dot products straight
-  // from HBM into G, then the bilinear.  Levels off the fast path (windows too
-  // spread for it), and fast-path levels with a non-finite tile (split-f16
-  // products: |feature| >= 65520, or infinite / NaN features).
+  // from HBM into G, then the bilinear (levels off the fast path: windows too
+  // spread for it).
   auto raw_level = [&](int l) {
     const int H2 = LV_SEL(H2, l), W2 = LV_SEL(W2, l);
     const T* f2 = static_cast<const T*>(LV_SEL(f2, l)) + ((size_t)b * N2 + jx) * H2 * W2 * C;
@@ -561,7 +500,6 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   }
 
   if (nT > 0) {
-    bool bad = false;  // a non-finite split-f16 tile in the current level
     // Deferred G store: tile i's sums are written in step i + 1, after that
     // step's MFMAs are issued, so the wave never stalls on the chain it has
     // just issued (a level's last tile is stored at once, before the bilinear)
@@ -573,14 +511,13 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
       for (int r = 0; r < 4; r++) {
         const int row = 4 * aq + r;
         if (row < np) {
-          if constexpr (kHalf) G[row * kBoxStride + toff + ai] = a0[r] + a1[r];
-          else G[row * kBoxStride + toff + ai] = (a0[r] + a1[r] * (1.0f / 2048.0f)) * ainv;
+          G[row * kBoxStride + toff + ai] = a0[r] + a1[r];
         }
       }
     };
     auto step = [&](u32x4 (&cur)[V], int i) __attribute__((always_inline)) {
       const bool live = i < nT;  // the last group may hold 1-2 slots past the end
-      // the tile's G values: fp16 acc0 + acc1; fp32 (acc0 + acc1 2^-11) 2^ae
+      // the tile's G values: acc0 + acc1
       f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
       auto mma = [&](const u32x4 (&B)[V]) __attribute__((always_inline)) {
         if constexpr (kHalf) {
@@ -594,60 +531,9 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
             if (h & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8, b8, acc1, 0, 0, 0);
             else acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a8, b8, acc0, 0, 0, 0);
           }
-        } else {
-          // fp32 features, split-f16 products (VERDICT r04 item 3 option 2):
-          // b = bh + bl with bh = f16(b), bl = f16(b - bh) (RNE), and per edge
-          // a = (ah + al' 2^-11) 2^ae (al' = f16((a - ah) 2^11), build_A);
-          //   a b 2^-ae = ah bh + ah bl + (al' bh) 2^-11   (+ al bl, dropped)
-          // Each f16 x f16 product is exact in fp32 and v_mfma_f32_16x16x32_f16
-          // accumulates in fp32: per product |err| <= 2^-21 |a||b| + 2^-25 |a|
-          // (bl below the f16 normal range for |b| < 2^-3), against 2^-24
-          // per fp32 rounding.  12 MFMAs of 16 cycles per tile
-          // instead of 32 v_mfma_f32_16x16x4_f32 of 32.  |b| >= 65520 makes
-          // bh infinite: a tile whose sums come out non-finite is redone on
-          // the scalar fp32 path (raw_level), which also gives the fp32
-          // result for infinite / NaN features.
-#pragma unroll
-          for (int t = 0; t < 4; t++) {
-            const float4 c0 = __builtin_bit_cast(float4, B[2 * t]);
-            const float4 c1 = __builtin_bit_cast(float4, B[2 * t + 1]);
-            const float x[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-            f16x8 bh, bl;
-#ifdef CORR_DIAG_NO_CONV  // diagnostic builds only: the tile's two 16-B pieces taken as
-                          // ready f16 halves (the loads of a pre-split pyramid, no conversion)
-            (void)x;
-            bh = __builtin_bit_cast(f16x8, B[2 * t]);
-            bl = __builtin_bit_cast(f16x8, B[2 * t + 1]);
-#else
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-              const _Float16 hv = (_Float16)x[j];
-              bh[j] = hv;
-              bl[j] = (_Float16)(x[j] - (float)hv);
-            }
-#endif
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah[t], bh, acc0, 0, 0, 0);
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah[t], bl, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Alds[t * kWave + lane], bh, acc1, 0, 0, 0);
-          }
-#ifdef CORR_DIAG_NO_CONV
-          const bool fin = true;
-#else
-          const bool fin = __builtin_isfinite(acc0[0] + acc0[1] + acc0[2] + acc0[3] + acc1[0] +
-                                              acc1[1] + acc1[2] + acc1[3]);
-#endif
-          bad = bad || __builtin_amdgcn_ballot_w64(!fin) != 0;
         }
       };
-      CORR_TSTAMP(i, 0);
-#ifndef CORR_DIAG_NO_MMA  // diagnostic builds only (timing of the rest of the tile loop)
       if (live) mma(cur);
-#else
-      if (live) {
-        acc0[0] = __builtin_bit_cast(float, cur[0].x);
-        acc1[0] = __builtin_bit_cast(float, cur[V - 1].w);
-      }
-#endif
       if (pgoff >= 0) {  // the previous tile's sums (its MFMA chain has drained)
         store_g(pg0, pg1, pgoff);
         pgoff = -1;
@@ -658,7 +544,6 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
         // same load order and the wait before a tile drains only that tile's loads
         load_tile(cur, i + kRing);
       }
-      CORR_TSTAMP(i, 1);
       if (!live) return;
       const TileDesc& d = td[pos_of(i)];
       const int t = i - d.c0, l = wave_uniform(d.lvl);
@@ -668,19 +553,11 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
         pg1 = acc1;
         pgoff = wave_uniform(16 * t);
       }
-      CORR_TSTAMP(i, 2);
       if (lend) {  // level complete: its last sums, the bilinear, then G is free again
         store_g(acc0, acc1, 16 * t);
-        CORR_STAMP(2 + 2 * l);
-        if (bad) {  // rare: redo the level on the scalar fp32 path
-          raw_level(l);
-          bad = false;
-        } else {
-          wave_lds_sync();
-          bilinear(l, true);
-          wave_lds_sync();
-        }
-        CORR_STAMP(3 + 2 * l);
+        wave_lds_sync();
+        bilinear(l, true);
+        wave_lds_sync();
       }
     };
     // no early exit inside a group: a break path into the loop's flow block
@@ -692,7 +569,6 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   }
 
   // ---- one contiguous [nout][L] row block per edge
-  CORR_STAMP(10);
   float* dst = out + ((size_t)b * M + m) * nout * L;
   wave_lds_sync();
   if (((nout * L) & 3) == 0) {  // whole float4s; the block start is 16-B aligned then too
@@ -701,8 +577,6 @@ __global__ void __launch_bounds__(kNhwcWaves* kWave, 2)  // 2 workgroups (8 wave
   } else {
     for (int e = lane; e < nout * L; e += kWave) dst[e] = obuf[e];
   }
-  CORR_STAMP(11);
-  CORR_STAMP_RT(13);
 }
 
 // ---------------------------------------------------------------------------
@@ -739,10 +613,6 @@ __host__ __device__ inline int corr_lvl_wave_bytes(int np) {
   return (int)(sizeof(float) * np * kLvlBoxStride + kLvlStage + sizeof(LvlGeom));
 }
 
-#ifndef LVL_STAMP
-#define LVL_STAMP_INIT
-#define LVL_STAMP(k)
-#endif
 // RAW9: p = 3, R = 3 (DPVO) as compile-time constants; otherwise run-time np, R
 template <int RING, bool RAW9>
 __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_eu(RING > 2 ? 3 : 4)))
@@ -754,7 +624,6 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
   const int np = RAW9 ? 9 : np_, R = RAW9 ? 3 : R_;
   const int w = wave_uniform(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
   const int C = kNhwcC, D = 2 * R + 2, Dp = D - 1, nout = Dp * Dp * np;
-  LVL_STAMP_INIT;
   char* wl = reinterpret_cast<char*>(smem) + (size_t)w * corr_lvl_wave_bytes(np);
   float* G = reinterpret_cast<float*>(wl);
   char* stage = wl + sizeof(float) * np * kLvlBoxStride;
@@ -771,7 +640,6 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
 
   // ---- one (edge position p, level lev) unit
   auto run_unit = [&](int p, int lev) __attribute__((always_inline)) {
-    LVL_STAMP(0);
     const int edge = order ? wave_uniform(order[p]) : p;
     const int b = edge / M, m = edge % M;
     const int ix = wave_uniform((int)ii[m]), jx = wave_uniform((int)jj[m]);
@@ -1002,7 +870,6 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
         d[h] = *reinterpret_cast<const gu32x4*>(reinterpret_cast<uintptr_t>(s[h & 1] + 32 * (h >> 1)));
     };
     u32x4 ring[RING][8];
-    LVL_STAMP(1);
     // unconditional preload (an empty box reads the frame's first pixel): the
     // waits below then count exactly
 #pragma unroll
@@ -1010,7 +877,6 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
       load_tile(ring[k], k);
       __builtin_amdgcn_sched_barrier(0);
     }
-    LVL_STAMP(2);
 
     // A fragments: lane (i = lane & 15, q = lane >> 4) holds patch row i,
     // channels 16 h + 4 q + s at a[4 h + s] (zero for rows i >= np)
@@ -1030,7 +896,6 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
         }
       wave_lds_sync();  // G free again
     }
-    LVL_STAMP(3);
 
     // stage addresses: a lane writes its 16 B of pixel pt = 8 ph + (lane >> 3),
     // chunk c = lane & 7 at pt * 128 + ((c ^ (pt & 7)) * 16); B fragment of
@@ -1073,16 +938,11 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
     };
     for (int t = 0; t < ntile; t += RING) {
 #pragma unroll
-      for (int k = 0; k < RING; k++) {
-        step(ring[k], t + k);
-        if (t + k == 0) LVL_STAMP(4);
-      }
+      for (int k = 0; k < RING; k++) step(ring[k], t + k);
     }
-    LVL_STAMP(5);
     wave_lds_sync();
     bilinear_store(true);
     wave_lds_sync();  // G, stage and geo free for the next unit
-    LVL_STAMP(6);
   };
 
   if (w < L) {
@@ -1137,14 +997,6 @@ __global__ void __launch_bounds__(256)
 
 using namespace dpvo;
 
-// experiment switch (A/B of the per-edge and the per-level kernels)
-static int g_corr_variant = 1;
-DPVO_EXPORT int dpvo_corr_nhwc_variant(int v) {
-  const int old = g_corr_variant;
-  if (v >= 0) g_corr_variant = v;
-  return old;
-}
-
 DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
     const void* fmap1, const void* const* fmap2, const int* H2, const int* W2, const float* scale,
     int L, const float* coords, const int64_t* ii, const int64_t* jj, const int32_t* order, int B,
@@ -1171,21 +1023,19 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   const bool ordered = order && B == 1;
   const int* ord = ordered ? (const int*)order : (const int*)nullptr;
   hipStream_t st = as_stream(stream);
-  if (g_corr_variant != 0 && dtype == DPVO_F32) {
-    // one wave per (edge, level) unit, two units per wave, whole-line tiles
+  if (dtype == DPVO_F32) {
+    // fp32: one wave per (edge, level) unit, two units per wave, whole-line
+    // tiles, exact fp32 products
     const size_t lsm = (size_t)L * corr_lvl_wave_bytes(np);
     const unsigned per = ordered ? (unsigned)((M + 7) / 8) : (unsigned)(B * M);
     const unsigned lg = ordered ? 8u * ((per + 1) / 2) : (per + 1) / 2;
-    const bool r9 = np == 9 && radius == 3;
-#define LVL_LAUNCH(RG, R9)                                                                       \
-  hipLaunchKernelGGL((corr_nhwc_lvl_kernel<RG, R9>), dim3(lg), dim3(L * kWave), lsm, st,         \
-                     (const float*)fmap1, lv, L, coords, ii, jj, B, M, np, N1, N2, radius, ord, out)
-    if (g_corr_variant == 3) {
-      if (r9) LVL_LAUNCH(3, true); else LVL_LAUNCH(3, false);
-    } else {
-      if (r9) LVL_LAUNCH(2, true); else LVL_LAUNCH(2, false);
-    }
-#undef LVL_LAUNCH
+    const dim3 g(lg), blk(L * kWave);
+    if (np == 9 && radius == 3)
+      hipLaunchKernelGGL((corr_nhwc_lvl_kernel<2, true>), g, blk, lsm, st, (const float*)fmap1, lv,
+                         L, coords, ii, jj, B, M, np, N1, N2, radius, ord, out);
+    else
+      hipLaunchKernelGGL((corr_nhwc_lvl_kernel<2, false>), g, blk, lsm, st, (const float*)fmap1, lv,
+                         L, coords, ii, jj, B, M, np, N1, N2, radius, ord, out);
     return launch_status();
   }
   const size_t smem = corr_nhwc_lds_bytes(np, radius, L);
@@ -1194,23 +1044,13 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   if (ordered) grid = 8u * (unsigned)((grid + 7) / 8);
   const bool raw9 = np == 9 && radius == 3;  // DPVO: p = 3, R = 3
   const dim3 g(grid), blk(kNhwcWaves * kWave);
-  if (dtype == DPVO_F16) {
-    const __half* f1 = (const __half*)fmap1;
-    if (raw9)
-      hipLaunchKernelGGL((corr_nhwc_kernel<__half, true>), g, blk, smem, st, f1, lv, L, coords, ii,
-                         jj, B, M, np, N1, N2, radius, ord, out);
-    else
-      hipLaunchKernelGGL((corr_nhwc_kernel<__half, false>), g, blk, smem, st, f1, lv, L, coords,
-                         ii, jj, B, M, np, N1, N2, radius, ord, out);
-  } else {
-    const float* f1 = (const float*)fmap1;
-    if (raw9)
-      hipLaunchKernelGGL((corr_nhwc_kernel<float, true>), g, blk, smem, st, f1, lv, L, coords, ii,
-                         jj, B, M, np, N1, N2, radius, ord, out);
-    else
-      hipLaunchKernelGGL((corr_nhwc_kernel<float, false>), g, blk, smem, st, f1, lv, L, coords,
-                         ii, jj, B, M, np, N1, N2, radius, ord, out);
-  }
+  const __half* f1 = (const __half*)fmap1;
+  if (raw9)
+    hipLaunchKernelGGL((corr_nhwc_kernel<__half, true>), g, blk, smem, st, f1, lv, L, coords, ii,
+                       jj, B, M, np, N1, N2, radius, ord, out);
+  else
+    hipLaunchKernelGGL((corr_nhwc_kernel<__half, false>), g, blk, smem, st, f1, lv, L, coords, ii,
+                       jj, B, M, np, N1, N2, radius, ord, out);
   return launch_status();
 }
 

@@ -16,10 +16,9 @@
 #   phases     BA window phase tables: cfg2 2 iterations, DPVO windows E=9850 / 3940 1 iteration
 #   probe      host enqueue time per call of a step, first after a sync vs steady
 #   stale      the stale-granule regression test; staledemo: its A/B on the round-4 tree
-#   corrmicro  A-CORR micro-bench (per-wave phase stamps) for each built variant
 #   launchprof rocprof kernel durations of the fused start-of-update launch and its parts
-#   corrvar    A-CORR kernel variants (scripts/corr_variants.py): time + deviation
-#   corrpmc    SQ / TCC counter passes over the corr variants (scripts/pmc_corrvar.sh)
+#   corrvar    A-CORR product kernel times, fp32 and fp16 (scripts/corr_variants.py)
+#   corrpmc    SQ / TCC counter passes over scripts/corr_variants.py (scripts/pmc_corrvar.sh)
 #   corrwide   the channels-last corr tests incl. the wide-dynamic-range ones
 #   cfg4       bench.py --sharded (cfg4 global BA, one rank)
 #   cfg4prof   rocprofv3 over the cfg4 bench
@@ -67,10 +66,6 @@ for s in "$@"; do
     probe) run probe 300 python -u scripts/host_enqueue_probe.py ;;
     staledemo) run staledemo 400 python -u scripts/stale_granule_demo.py _r04tree . ;;
     stale) run stale 400 $PYT tests/test_granule_stale_gpu.py ;;
-    corrmicro)  # scripts/micro/corr_bench variants (build them first on the CPU side)
-      for v in ${CORR_VARIANTS:-base exact nomma noload}; do
-        run corrmicro_$v 200 ./scripts/micro/corr_bench_$v 1 0 4 2048
-      done ;;
     launchprof)  # kernel durations of the update's first launch and its parts
       run launchprof 300 rocprofv3 --kernel-trace --stats -d $O/${T}_launchprof -o run --output-format csv \
         -- python scripts/reproject_launch_bench.py cfg2 dpvo25
