@@ -1,7 +1,7 @@
 """A-CORR product kernels on the bench's exact cfg2 call (channels-last
 pyramid, levels [1,2,4,8], 2048 edges, XCD order): HIP-event median per
 launch for fp32 features (corr_nhwc_lvl_kernel, exact fp32 products) and fp16
-features (corr_nhwc_kernel), and the max deviation from the fp64 oracle on a
+features (the same kernel, fp16 MFMA), and the max deviation from the fp64 oracle on a
 sample of edges.
 
     python scripts/corr_variants.py [--reps 200] [--features f32,f16]
