@@ -84,9 +84,14 @@ struct LvlGeom {
   int x0[kNpMax], y0[kNpMax];
   float dx[kNpMax], dy[kNpMax];
 };
-// per wave: G [np][kLvlBoxStride] floats, the stage, the geometry
-__host__ __device__ inline int corr_lvl_wave_bytes(int np) {
-  return (int)(sizeof(float) * np * kLvlBoxStride + kLvlStage + sizeof(LvlGeom));
+// per wave: G [np][kLvlBoxStride] floats, the stage, the geometry, the
+// first unit's output slice (nout floats; the second unit's stays in the stage)
+__host__ __device__ inline int corr_lvl_out_bytes(int np, int R) {
+  return ((2 * R + 1) * (2 * R + 1) * np * (int)sizeof(float) + 15) & ~15;
+}
+__host__ __device__ inline int corr_lvl_wave_bytes(int np, int R) {
+  return (int)(sizeof(float) * np * kLvlBoxStride + kLvlStage + sizeof(LvlGeom)) +
+         corr_lvl_out_bytes(np, R);
 }
 
 // RAW9: p = 3, R = 3 (DPVO) as compile-time constants; otherwise run-time np, R
@@ -103,10 +108,14 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
   const int np = RAW9 ? 9 : np_, R = RAW9 ? 3 : R_;
   const int w = wave_uniform(threadIdx.x / kWave), lane = threadIdx.x & (kWave - 1);
   const int C = kNhwcC, D = 2 * R + 2, Dp = D - 1, nout = Dp * Dp * np;
-  char* wl = reinterpret_cast<char*>(smem) + (size_t)w * corr_lvl_wave_bytes(np);
+  const int wbytes = corr_lvl_wave_bytes(np, R);
+  char* wl = reinterpret_cast<char*>(smem) + (size_t)w * wbytes;
   float* G = reinterpret_cast<float*>(wl);
   char* stage = wl + sizeof(float) * np * kLvlBoxStride;
   LvlGeom* geo = reinterpret_cast<LvlGeom*>(stage + kLvlStage);
+  // output slices: unit 0 (level w of edge A) in its own region, unit 1
+  // (level L-1-w of edge B) in the stage, stored by the workgroup at the end
+  float* outA = reinterpret_cast<float*>(geo + 1);
   const int ai = lane & 15, aq = lane >> 4;
 
   // edge positions of this workgroup: with an order (B == 1, XCD-aware) XCD
@@ -118,7 +127,7 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
   if (j8 >= half) return;
 
   // ---- one (edge position p, level lev) unit
-  auto run_unit = [&](int p, int lev) __attribute__((always_inline)) {
+  auto run_unit = [&](int p, int lev, float* so) __attribute__((always_inline)) {
     const int edge = order ? wave_uniform(order[p]) : p;
     const int b = edge / M, m = edge % M;
     const int ix = wave_uniform((int)ii[m]), jx = wave_uniform((int)jj[m]);
@@ -211,11 +220,9 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
     }
     const int ntile = (bw * bh + 15) >> 4;
     const bool fast = ntile <= kLvlMaxTiles;
-    float* dst = out + ((size_t)b * M + m) * nout * L + lev;
 
-    // bilinear + permute from G (correlation_kernel.cu:260-271), then this
-    // level's slice of the edge's [nout][L] block straight to HBM: output o
-    // of lane o % 64 (consecutive outputs in consecutive lanes, 16 B apart)
+    // bilinear + permute from G (correlation_kernel.cu:260-271) into this
+    // level's output slice so[nout] in LDS (output order)
     auto tap4 = [&](int k, int yy, int xx, bool mat, float& r00, float& r01, float& r10,
                     float& r11) __attribute__((always_inline)) {
       if (mat) {  // clamped (valid) LDS addresses, zeroed by a select
@@ -275,19 +282,10 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
             v[k] = bil(k, r00, r01, r10, r11);
           }
         }
-        float* so = reinterpret_cast<float*>(stage);
         if (on) {
 #pragma unroll
           for (int k = 0; k < 9; k++) so[(xx * Dp + yy) * 9 + k] = v[k];
         }
-        wave_lds_sync();
-#pragma unroll
-        for (int u = 0; u < 7; u++) {
-          const int o = lane + kWave * u;
-          const float vo = so[min(o, 440)];
-          if (o < 441) dst[(size_t)o * L] = vo;
-        }
-        wave_lds_sync();  // stage free again
       } else {
 #pragma unroll
         for (int u = 0; u < kOutPerLane; u++) {
@@ -297,7 +295,7 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
           float r00, r01, r10, r11;
           tap4(k, yy, xx, mat, r00, r01, r10, r11);
           const float v = bil(k, r00, r01, r10, r11);
-          if (o < nout) dst[(size_t)o * L] = v;
+          if (o < nout) so[o] = v;
         }
       }
     };
@@ -320,7 +318,7 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
       }
       wave_lds_sync();
       bilinear_store(false);
-      wave_lds_sync();
+      wave_lds_sync();  // G free
       return;
     }
 
@@ -453,11 +451,41 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
     wave_lds_sync();  // G, stage and geo free for the next unit
   };
 
-  if (w < L) {
-    const int pA = x8 * per + j8, pB = pA + half;
-    const int lim = order ? min(per * (x8 + 1), M) : nE;
-    if (pA < lim) run_unit(pA, w);
-    if (pB < lim && pB < x8 * per + per) run_unit(pB, L - 1 - w);
+  const int pA = x8 * per + j8, pB = pA + half;
+  const int lim = order ? min(per * (x8 + 1), M) : nE;
+  const bool okA = pA < lim, okB = pB < lim && pB < x8 * per + per;
+  float* const sB = reinterpret_cast<float*>(stage);
+  if (okA) run_unit(pA, w, outA);
+  if (okB) run_unit(pB, L - 1 - w, sB);
+
+  // the two edges' [nout][L] blocks from the waves' slices: whole lines,
+  // 16 B per lane when the block is a whole number of 16-B pieces
+  __syncthreads();
+  const int nl = nout * L, tid = threadIdx.x, nth = L * kWave;
+#pragma unroll
+  for (int u = 0; u < 2; u++) {
+    if (!(u == 0 ? okA : okB)) continue;
+    const int edge = order ? wave_uniform(order[u == 0 ? pA : pB]) : (u == 0 ? pA : pB);
+    float* dst = out + (size_t)edge * nl;
+    // level l of edge A is in wave l's region, of edge B in wave L-1-l's stage
+    const int off = u == 0 ? (int)(reinterpret_cast<char*>(outA) - wl) : (int)(stage - wl);
+    auto slice = [&](int l) -> const float* {
+      const int wv = u == 0 ? l : L - 1 - l;
+      return reinterpret_cast<const float*>(reinterpret_cast<const char*>(smem) + wv * wbytes + off);
+    };
+    if (L == kMaxL && (nl & 3) == 0) {
+      const float* s0 = slice(0);
+      const float* s1 = slice(1);
+      const float* s2 = slice(2);
+      const float* s3 = slice(3);
+      for (int o = tid; o < nout; o += nth)
+        *reinterpret_cast<float4*>(dst + 4 * o) = make_float4(s0[o], s1[o], s2[o], s3[o]);
+    } else {
+      for (int e = tid; e < nl; e += nth) {
+        const int o = e / L, l = e - o * L;
+        dst[e] = slice(l)[o];
+      }
+    }
   }
 }
 
@@ -532,7 +560,7 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   const int* ord = ordered ? (const int*)order : (const int*)nullptr;
   hipStream_t st = as_stream(stream);
   // one wave per (edge, level) unit, two units per wave, whole-line tiles
-  const size_t lsm = (size_t)L * corr_lvl_wave_bytes(np);
+  const size_t lsm = (size_t)L * corr_lvl_wave_bytes(np, radius);
   const unsigned per = ordered ? (unsigned)((M + 7) / 8) : (unsigned)(B * M);
   const unsigned lg = ordered ? 8u * ((per + 1) / 2) : (per + 1) / 2;
   const dim3 g(lg), blk(L * kWave);

@@ -4,7 +4,10 @@ launch for fp32 features (corr_nhwc_lvl_kernel, exact fp32 products) and fp16
 features (the same kernel, fp16 MFMA), and the max deviation from the fp64 oracle on a
 sample of edges.
 
-    python scripts/corr_variants.py [--reps 200] [--features f32,f16]
+    python scripts/corr_variants.py [--reps 200] [--features f32,f16] [--native DIR]
+
+--native DIR loads the extension modules from another build directory (a
+copy of dpvo_amd/_native built from another tree) for A/B runs in one call.
 
 (Round 6's A/B of the per-edge split-f16 kernel against the per-level kernel
 is in profiles/r06_mid/corr_variants.txt.)
@@ -21,6 +24,11 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+import dpvo_amd._native as _nat  # noqa: E402
+
+if "--native" in sys.argv:
+    _nat.NATIVE_DIR = os.path.abspath(sys.argv[sys.argv.index("--native") + 1])
+
 from dpvo_amd import altcorr, fastba, synthetic  # noqa: E402
 
 
@@ -29,6 +37,7 @@ def main():
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--features", default="f32,f16")
     ap.add_argument("--levels", default="1,2,4,8")
+    ap.add_argument("--native", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     G = synthetic.make_config("cfg2", seed=0)
@@ -71,7 +80,7 @@ def main():
             dev_max = worst
         except Exception as e:  # the oracle is a checker only; timing stands without it
             dev_max = f"oracle unavailable: {e}"
-        print(json.dumps({"features": feat, "levels": levels, "us_median": ts[len(ts) // 2],
+        print(json.dumps({"native": args.native or "in-tree", "features": feat, "levels": levels, "us_median": ts[len(ts) // 2],
                           "us_min": ts[0], "max_dev_vs_oracle_rel_sample": dev_max}), flush=True)
 
 
