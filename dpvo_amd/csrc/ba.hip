@@ -416,7 +416,8 @@ __global__ void reproject_kernel(const float* __restrict__ poses, const float* _
                                  int* __restrict__ order, int N2) {
   if (order && blockIdx.x == gridDim.x - 1) {  // extra workgroup: A-CORR edge order
     __shared__ int bins[kOrderBins + 1];
-    edge_order_block(jj, E, N2, order, bins);
+    const OrderIn q{poses, patches, intrinsics, ii, kk, P, num_poses, num_patches};
+    edge_order_block(q, jj, E, N2, order, bins);
     return;
   }
   const int PP = P * P;

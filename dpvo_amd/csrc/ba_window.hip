@@ -709,7 +709,8 @@ __global__ void __launch_bounds__(kPT) reproject_plan_kernel(RArgs R, Plan plan)
     return;
   }
   if ((int)blockIdx.x == R.nps) {
-    edge_order_block(R.jj, R.E, R.N2, R.order, reinterpret_cast<int*>(lds));
+    const OrderIn q{R.poses, R.patches, R.intrinsics, R.ii, R.kk, R.P, R.num_poses, R.num_patches};
+    edge_order_block(q, R.jj, R.E, R.N2, R.order, reinterpret_cast<int*>(lds));
     return;
   }
   const int PP = R.P * R.P;
@@ -744,7 +745,8 @@ __device__ __forceinline__ void reproject_plan_insert_body(const RArgs& R, const
     return;
   }
   if (b == R.nps) {
-    edge_order_block(R.jj, R.E, R.N2, R.order, reinterpret_cast<int*>(lds));
+    const OrderIn q{R.poses, R.patches, R.intrinsics, R.ii, R.kk, R.P, R.num_poses, R.num_patches};
+    edge_order_block(q, R.jj, R.E, R.N2, R.order, reinterpret_cast<int*>(lds));
     return;
   }
   if (b < b0 + nrep) {

@@ -99,46 +99,6 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
-// --- edge order by target frame (XCD-aware A-CORR scheduling) -------------------
-// One workgroup: order[p] = the edge at position p when edges are grouped by
-// their target frame jj (counting sort; the order inside a group is whatever
-// the LDS atomics give -- A-CORR results do not depend on it, every edge is
-// computed independently).  bins: >= kOrderBins + 1 ints of LDS.  Keys outside
-// [0, min(N2, kOrderBins)) share the last bin.
-constexpr int kOrderBins = 1024;
-__device__ inline void edge_order_block(const int64_t* __restrict__ jj, int E, int N2,
-                                        int* __restrict__ order, int* bins) {
-  const int tid = threadIdx.x, T = blockDim.x;
-  const int nb = min(max(N2, 1), kOrderBins);
-  for (int b = tid; b <= nb; b += T) bins[b] = 0;
-  __syncthreads();
-  for (int e = tid; e < E; e += T) {
-    const int64_t v = jj[e];
-    atomicAdd(&bins[(v >= 0 && v < nb) ? (int)v : nb - 1], 1);
-  }
-  __syncthreads();
-  if (tid < 64) {  // exclusive scan of nb <= 1024 bins by one wave
-    int carry = 0;
-    for (int b0 = 0; b0 < nb; b0 += 64) {
-      const int b = b0 + tid;
-      const int c = (b < nb) ? bins[b] : 0;
-      int x = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (tid >= o) x += y;
-      }
-      if (b < nb) bins[b] = carry + x - c;
-      carry += __shfl(x, 63, 64);
-    }
-  }
-  __syncthreads();
-  for (int e = tid; e < E; e += T) {
-    const int64_t v = jj[e];
-    order[atomicAdd(&bins[(v >= 0 && v < nb) ? (int)v : nb - 1], 1)] = e;
-  }
-}
-
 // --- fp32 SE3 primitives of ba_cuda.cu:36-174 (restated, device) ---------------
 // No FMA contraction here: the per-edge arithmetic then rounds exactly like the
 // C oracle (x86, no FMA), which keeps the parity tests tight.
@@ -258,14 +218,14 @@ __device__ __forceinline__ void retrSE3(const float* xi, const float* t, const f
 // F-REPROJ of one (edge n, patch pixel pix) (ba_cuda.cu:379-429): shared by
 // reproject_kernel (ba.hip) and the fused reproject + BA-plan launch
 // (ba_window.hip), so both round identically.
-__device__ __forceinline__ void reproject_pixel(const float* __restrict__ poses,
-                                                const float* __restrict__ patches,
-                                                const float* __restrict__ intrinsics,
-                                                const int64_t* __restrict__ ii,
-                                                const int64_t* __restrict__ jj,
-                                                const int64_t* __restrict__ kk, int n, int pix,
-                                                int P, int num_poses, int num_patches,
-                                                float* __restrict__ coords) {
+// reprojected pixel (u, v) of patch pixel `pix` of edge n (ba_cuda.cu:379-429)
+__device__ __forceinline__ void reproject_uv(const float* __restrict__ poses,
+                                             const float* __restrict__ patches,
+                                             const float* __restrict__ intrinsics,
+                                             const int64_t* __restrict__ ii,
+                                             const int64_t* __restrict__ jj,
+                                             const int64_t* __restrict__ kk, int n, int pix, int P,
+                                             int num_poses, int num_patches, float& u, float& v) {
   const int PP = P * P;
   const float fx = intrinsics[0], fy = intrinsics[1], cx = intrinsics[2], cy = intrinsics[3];
   const int ix = (int)min(max(ii[n], (int64_t)0), (int64_t)num_poses - 1);
@@ -284,10 +244,84 @@ __device__ __forceinline__ void reproject_pixel(const float* __restrict__ poses,
   Xi[2] = 1.0f;
   Xi[3] = pk[2 * PP + pix];
   actSE3(tij, qij, Xi, Xj);
-  coords[((size_t)n * 2 + 0) * PP + pix] = fx * (Xj[0] / Xj[2]) + cx;
-  coords[((size_t)n * 2 + 1) * PP + pix] = fy * (Xj[1] / Xj[2]) + cy;
+  u = fx * (Xj[0] / Xj[2]) + cx;
+  v = fy * (Xj[1] / Xj[2]) + cy;
+}
+
+__device__ __forceinline__ void reproject_pixel(const float* __restrict__ poses,
+                                                const float* __restrict__ patches,
+                                                const float* __restrict__ intrinsics,
+                                                const int64_t* __restrict__ ii,
+                                                const int64_t* __restrict__ jj,
+                                                const int64_t* __restrict__ kk, int n, int pix,
+                                                int P, int num_poses, int num_patches,
+                                                float* __restrict__ coords) {
+  const int PP = P * P;
+  float u, v;
+  reproject_uv(poses, patches, intrinsics, ii, jj, kk, n, pix, P, num_poses, num_patches, u, v);
+  coords[((size_t)n * 2 + 0) * PP + pix] = u;
+  coords[((size_t)n * 2 + 1) * PP + pix] = v;
 }
 
 #pragma clang fp contract(fast)
+
+// --- edge order for A-CORR (XCD-aware scheduling) -----------------------------
+// One workgroup: order[p] = the edge at position p when edges are grouped by
+// their target frame jj and, inside a frame, by the 16-pixel row band of the
+// reprojected patch centre (counting sort; the order inside a (frame, band)
+// bin is whatever the LDS atomics give -- A-CORR results do not depend on it,
+// every edge is computed independently).  A-CORR gives each XCD an eighth of
+// the positions: a frame's edges on one L2, and edges whose windows overlap
+// near each other in the sequence, so the waves that share box lines run at
+// the same time (cfg2 fp32: 41.3 -> 40.4 us, scripts/corr_order_probe.py).
+// The centre is recomputed in both passes (no per-edge LDS: E is unbounded
+// here).  bins: >= kOrderBins + 1 ints of LDS.  Frames outside
+// [0, min(N2, kOrderBins / kOrderBands)) share the last frame's bins.
+struct OrderIn {
+  const float* poses;
+  const float* patches;
+  const float* intrinsics;
+  const int64_t* ii;
+  const int64_t* kk;
+  int P, num_poses, num_patches;
+};
+constexpr int kOrderBins = 1024;
+constexpr int kOrderBands = 16;  // row bands of 16 level-1 pixels (rows >= 240 share the last)
+__device__ __forceinline__ int edge_order_key(const OrderIn& q, const int64_t* __restrict__ jj,
+                                              int e, int nf) {
+  const int64_t f = jj[e];
+  float u, v;
+  const int c = (q.P / 2) * q.P + q.P / 2;
+  reproject_uv(q.poses, q.patches, q.intrinsics, q.ii, jj, q.kk, e, c, q.P, q.num_poses,
+               q.num_patches, u, v);
+  const int band = v >= 0.0f ? (int)fminf(v * (1.0f / 16.0f), (float)(kOrderBands - 1)) : 0;  // NaN: 0
+  return ((f >= 0 && f < nf) ? (int)f : nf - 1) * kOrderBands + band;
+}
+__device__ inline void edge_order_block(const OrderIn& q, const int64_t* __restrict__ jj, int E,
+                                        int N2, int* __restrict__ order, int* bins) {
+  const int tid = threadIdx.x, T = blockDim.x;
+  const int nf = min(max(N2, 1), kOrderBins / kOrderBands), nb = nf * kOrderBands;
+  for (int b = tid; b <= nb; b += T) bins[b] = 0;
+  __syncthreads();
+  for (int e = tid; e < E; e += T) atomicAdd(&bins[edge_order_key(q, jj, e, nf)], 1);
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of nb <= 1024 bins by one wave
+    int carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+      const int b = b0 + tid;
+      const int c = (b < nb) ? bins[b] : 0;
+      int x = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (tid >= o) x += y;
+      }
+      if (b < nb) bins[b] = carry + x - c;
+      carry += __shfl(x, 63, 64);
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < E; e += T) order[atomicAdd(&bins[edge_order_key(q, jj, e, nf)], 1)] = e;
+}
 
 }  // namespace dpvo

@@ -565,13 +565,13 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   const unsigned lg = ordered ? 8u * ((per + 1) / 2) : (per + 1) / 2;
   const dim3 g(lg), blk(L * kWave);
   const bool r9 = np == 9 && radius == 3;  // DPVO: p = 3, R = 3
-#define LVL_LAUNCH(TT, R9)                                                                  \
-  hipLaunchKernelGGL((corr_nhwc_lvl_kernel<TT, 2, R9>), g, blk, lsm, st, (const TT*)fmap1, lv, L, \
+#define LVL_LAUNCH(TT, RG, R9)                                                                \
+  hipLaunchKernelGGL((corr_nhwc_lvl_kernel<TT, RG, R9>), g, blk, lsm, st, (const TT*)fmap1, lv, L, \
                      coords, ii, jj, B, M, np, N1, N2, radius, ord, out)
   if (dtype == DPVO_F32) {
-    if (r9) LVL_LAUNCH(float, true); else LVL_LAUNCH(float, false);
+    if (r9) LVL_LAUNCH(float, 2, true); else LVL_LAUNCH(float, 2, false);
   } else {
-    if (r9) LVL_LAUNCH(__half, true); else LVL_LAUNCH(__half, false);
+    if (r9) LVL_LAUNCH(__half, 4, true); else LVL_LAUNCH(__half, 4, false);
   }
 #undef LVL_LAUNCH
   return launch_status();

@@ -18,6 +18,9 @@
 #   stale      the stale-granule regression test; staledemo: its A/B on the round-4 tree
 #   launchprof rocprof kernel durations of the fused start-of-update launch and its parts
 #   corrvar    A-CORR product kernel times, fp32 and fp16 (scripts/corr_variants.py)
+#   corrab     A/B of builds copied to scratch_ab/<v> (VARIANTS, scripts/corr_ab.sh)
+#   dropin     per-level NCHW / channels-last drop-in calls (scripts/corr_dropin_bench.py)
+#   benchf16   bench.py --features f16 (the fork's MIXED_PRECISION rings)
 #   corrpmc    SQ / TCC counter passes over scripts/corr_variants.py (scripts/pmc_corrvar.sh)
 #   corrwide   the channels-last corr tests incl. the wide-dynamic-range ones
 #   cfg4       bench.py --sharded (cfg4 global BA, one rank)
@@ -73,6 +76,9 @@ for s in "$@"; do
         | tee $O/${T}_launchprof_kstats.txt ;;
     corrvar) run corrvar 200 python -u scripts/corr_variants.py ${CORRVAR_ARGS:-} ;;
     corrpmc) run corrpmc 700 bash scripts/pmc_corrvar.sh ;;
+    corrab) run corrab 400 bash scripts/corr_ab.sh ;;
+    dropin) run dropin 300 python -u scripts/corr_dropin_bench.py ;;
+    benchf16) run benchf16 300 python -u bench.py --features f16 --no-cpu-baseline ;;
     corrwide) run corrwide 300 $PYT tests/test_corr_gpu.py -k "wide_range or channels_last" ;;
     cfg4) run cfg4 300 python -u bench.py --sharded --steps 5 --warmup 2 ;;
     cfg4prof) prof cfg4prof --sharded --steps 3 --warmup 1 ;;

@@ -305,6 +305,11 @@ def test_ordered_corr_matches_unordered(gpu):
     assert sorted(o.tolist()) == list(range(G.E))
     jj = G.jj.numpy()[o]
     assert (np.diff(jj) >= 0).all()  # grouped by target frame, groups in frame order
+    # inside a frame: by the 16-pixel row band of the reprojected patch centre
+    v = coords[0, :, 1, 1, 1].cpu().numpy()[o]
+    band = np.where(v >= 0, np.minimum(v / 16.0, 15.0), 0).astype(np.int64)
+    key = jj.astype(np.int64) * 16 + band
+    assert (np.diff(key) >= 0).all()
     levels = (1, 2, 4, 8)
     pyr = [synthetic.channels_last(p) for p in
            synthetic.make_features(mem=mem, C=128, levels=levels, seed=1, device=gpu)]
