@@ -571,7 +571,7 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   if (dtype == DPVO_F32) {
     if (r9) LVL_LAUNCH(float, 2, true); else LVL_LAUNCH(float, 2, false);
   } else {
-    if (r9) LVL_LAUNCH(__half, 4, true); else LVL_LAUNCH(__half, 4, false);
+    if (r9) LVL_LAUNCH(__half, 2, true); else LVL_LAUNCH(__half, 2, false);
   }
 #undef LVL_LAUNCH
   return launch_status();

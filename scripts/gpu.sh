@@ -21,6 +21,7 @@
 #   corrab     A/B of builds copied to scratch_ab/<v> (VARIANTS, scripts/corr_ab.sh)
 #   dropin     per-level NCHW / channels-last drop-in calls (scripts/corr_dropin_bench.py)
 #   benchf16   bench.py --features f16 (the fork's MIXED_PRECISION rings)
+#   dpvoprof   rocprofv3 over the fork's live BA call at E = 9850 (scripts/dpvo_window_call.py)
 #   corrpmc    SQ / TCC counter passes over scripts/corr_variants.py (scripts/pmc_corrvar.sh)
 #   corrwide   the channels-last corr tests incl. the wide-dynamic-range ones
 #   cfg4       bench.py --sharded (cfg4 global BA, one rank)
@@ -79,6 +80,12 @@ for s in "$@"; do
     corrab) run corrab 400 bash scripts/corr_ab.sh ;;
     dropin) run dropin 300 python -u scripts/corr_dropin_bench.py ;;
     benchf16) run benchf16 300 python -u bench.py --features f16 --no-cpu-baseline ;;
+    dpvoprof)
+      run dpvocall 200 python -u scripts/dpvo_window_call.py
+      run dpvoprof 300 rocprofv3 --kernel-trace --stats -d $O/${T}_dpvoprof -o run --output-format csv \
+        -- python scripts/dpvo_window_call.py
+      python scripts/kstats.py "$(find $O/${T}_dpvoprof -name '*kernel_stats.csv' | head -1)" 8 \
+        | tee $O/${T}_dpvoprof_kstats.txt ;;
     corrwide) run corrwide 300 $PYT tests/test_corr_gpu.py -k "wide_range or channels_last" ;;
     cfg4) run cfg4 300 python -u bench.py --sharded --steps 5 --warmup 2 ;;
     cfg4prof) prof cfg4prof --sharded --steps 3 --warmup 1 ;;
