@@ -301,9 +301,30 @@ __device__ inline void edge_order_block(const OrderIn& q, const int64_t* __restr
                                         int N2, int* __restrict__ order, int* bins) {
   const int tid = threadIdx.x, T = blockDim.x;
   const int nf = min(max(N2, 1), kOrderBins / kOrderBands), nb = nf * kOrderBands;
+  if (E <= 0) return;
+  // keys of 4 edges (tid + 4 T k + r T) at a time, every load of the four
+  // issued before the first use; the first group's keys stay in registers
+  // for the scatter pass (E <= 4 T: no recomputation, cfg2)
+  auto keys4 = [&](int e0, int (&k)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) k[r] = edge_order_key(q, jj, min(e0 + r * T, E - 1), nf);
+  };
+  int k0[4];
+  keys4(tid, k0);
   for (int b = tid; b <= nb; b += T) bins[b] = 0;
   __syncthreads();
-  for (int e = tid; e < E; e += T) atomicAdd(&bins[edge_order_key(q, jj, e, nf)], 1);
+  for (int e0 = tid; e0 < E; e0 += 4 * T) {
+    int k[4];
+    if (e0 == tid) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) k[r] = k0[r];
+    } else {
+      keys4(e0, k);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      if (e0 + r * T < E) atomicAdd(&bins[k[r]], 1);
+  }
   __syncthreads();
   if (tid < 64) {  // exclusive scan of nb <= 1024 bins by one wave
     int carry = 0;
@@ -321,7 +342,18 @@ __device__ inline void edge_order_block(const OrderIn& q, const int64_t* __restr
     }
   }
   __syncthreads();
-  for (int e = tid; e < E; e += T) order[atomicAdd(&bins[edge_order_key(q, jj, e, nf)], 1)] = e;
+  for (int e0 = tid; e0 < E; e0 += 4 * T) {
+    int k[4];
+    if (e0 == tid) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) k[r] = k0[r];
+    } else {
+      keys4(e0, k);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      if (e0 + r * T < E) order[atomicAdd(&bins[k[r]], 1)] = e0 + r * T;
+  }
 }
 
 }  // namespace dpvo
