@@ -89,6 +89,11 @@ struct LvlGeom {
 __host__ __device__ inline int corr_lvl_out_bytes(int np, int R) {
   return ((2 * R + 1) * (2 * R + 1) * np * (int)sizeof(float) + 15) & ~15;
 }
+// edge positions per workgroup: its npos x L waves hold the (edge, level)
+// units, one or two per wave (pairs: L >= 3, where one unit per wave would
+// not leave the whole grid resident at DPVO sizes)
+__host__ __device__ inline bool corr_lvl_paired(int L) { return L >= 3; }
+__host__ __device__ inline int corr_lvl_npos(int L) { return L >= 3 ? 1 : kMaxL / L; }
 __host__ __device__ inline int corr_lvl_wave_bytes(int np, int R) {
   return (int)(sizeof(float) * np * kLvlBoxStride + kLvlStage + sizeof(LvlGeom)) +
          corr_lvl_out_bytes(np, R);
@@ -98,7 +103,7 @@ __host__ __device__ inline int corr_lvl_wave_bytes(int np, int R) {
 // T = float: exact fp32 products (v_mfma_f32_16x16x4_f32); T = __half (the
 // fork's MIXED_PRECISION rings): f16 x f16 on v_mfma_f32_16x16x32_f16, fp32
 // accumulation (documented deviation: the reference accumulates in fp16)
-template <typename T, int RING, bool RAW9>
+template <typename T, int RING, bool RAW9, bool PAIRED>
 __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_eu(RING > 2 ? 3 : 4)))
     corr_nhwc_lvl_kernel(const T* __restrict__ fmap1, NhwcLevels lv, int L,
                          const float* __restrict__ coords, const int64_t* __restrict__ ii,
@@ -122,9 +127,13 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
   // x = blockIdx % 8 takes the x-th eighth of the edges grouped by target
   // frame, a workgroup two positions of it half an eighth apart
   const int nE = B * M;
-  const int per = order ? (M + 7) / 8 : nE, half = (per + 1) / 2;
+  // paired: a wave runs level l of position q and level L-1-l of position
+  // q + half (fine and coarse levels together); otherwise one unit per wave
+  constexpr bool paired = PAIRED;  // = corr_lvl_paired(L)
+  const int per = order ? (M + 7) / 8 : nE, half = paired ? (per + 1) / 2 : per;
   const int x8 = order ? (int)(blockIdx.x % 8) : 0, j8 = order ? (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  if (j8 >= half) return;
+  const int npair = PAIRED ? 1 : corr_lvl_npos(L);
+  if (j8 * npair >= half) return;
 
   // ---- one (edge position p, level lev) unit
   auto run_unit = [&](int p, int lev, float* so) __attribute__((always_inline)) {
@@ -451,26 +460,37 @@ __global__ void __launch_bounds__(kMaxL* kWave) __attribute__((amdgpu_waves_per_
     wave_lds_sync();  // G, stage and geo free for the next unit
   };
 
-  const int pA = x8 * per + j8, pB = pA + half;
+  // wave w: pair sp = w / L, level lw = w % L of its first edge, L-1-lw of its second
   const int lim = order ? min(per * (x8 + 1), M) : nE;
-  const bool okA = pA < lim, okB = pB < lim && pB < x8 * per + per;
-  float* const sB = reinterpret_cast<float*>(stage);
-  if (okA) run_unit(pA, w, outA);
-  if (okB) run_unit(pB, L - 1 - w, sB);
+  auto pair_ok = [&](int q, int u) {
+    const int pa = x8 * per + q;
+    return q < half && (u == 0 ? pa < lim
+                               : (paired && pa + half < lim && pa + half < x8 * per + per));
+  };
+  {
+    const int sp = PAIRED ? 0 : w / L, lw = w - sp * L, q = j8 * npair + sp;
+    const int pA = x8 * per + q;
+    if (pair_ok(q, 0)) run_unit(pA, lw, outA);
+    if (pair_ok(q, 1)) run_unit(pA + half, L - 1 - lw, reinterpret_cast<float*>(stage));
+  }
 
-  // the two edges' [nout][L] blocks from the waves' slices: whole lines,
-  // 16 B per lane when the block is a whole number of 16-B pieces
+  // the edges' [nout][L] blocks from the waves' slices: whole lines, 16 B per
+  // lane when the block is a whole number of 16-B pieces
   __syncthreads();
-  const int nl = nout * L, tid = threadIdx.x, nth = L * kWave;
+  const int nl = nout * L, tid = threadIdx.x, nth = npair * L * kWave;
 #pragma unroll
-  for (int u = 0; u < 2; u++) {
-    if (!(u == 0 ? okA : okB)) continue;
-    const int edge = order ? wave_uniform(order[u == 0 ? pA : pB]) : (u == 0 ? pA : pB);
+  for (int u2 = 0; u2 < (PAIRED ? 2 : 2 * kMaxL); u2++) {
+    const int sp = u2 >> 1, u = u2 & 1, q = j8 * npair + sp;
+    if (sp >= npair) break;
+    if (!pair_ok(q, u)) continue;
+    const int pos = x8 * per + q + (u ? half : 0);
+    const int edge = order ? wave_uniform(order[pos]) : pos;
     float* dst = out + (size_t)edge * nl;
-    // level l of edge A is in wave l's region, of edge B in wave L-1-l's stage
+    // level l of the pair's first edge is in wave sp L + l's own region, of
+    // its second edge in wave sp L + L-1-l's stage
     const int off = u == 0 ? (int)(reinterpret_cast<char*>(outA) - wl) : (int)(stage - wl);
     auto slice = [&](int l) -> const float* {
-      const int wv = u == 0 ? l : L - 1 - l;
+      const int wv = sp * L + (u == 0 ? l : L - 1 - l);
       return reinterpret_cast<const float*>(reinterpret_cast<const char*>(smem) + wv * wbytes + off);
     };
     if (L == kMaxL && (nl & 3) == 0) {
@@ -560,19 +580,25 @@ DPVO_EXPORT int dpvo_corr_forward_levels_nhwc_ordered(
   const int* ord = ordered ? (const int*)order : (const int*)nullptr;
   hipStream_t st = as_stream(stream);
   // one wave per (edge, level) unit, two units per wave, whole-line tiles
-  const size_t lsm = (size_t)L * corr_lvl_wave_bytes(np, radius);
+  const int npair = corr_lvl_npos(L);
+  const size_t lsm = (size_t)npair * L * corr_lvl_wave_bytes(np, radius);
   const unsigned per = ordered ? (unsigned)((M + 7) / 8) : (unsigned)(B * M);
-  const unsigned lg = ordered ? 8u * ((per + 1) / 2) : (per + 1) / 2;
-  const dim3 g(lg), blk(L * kWave);
+  const unsigned nwg = ((corr_lvl_paired(L) ? (per + 1) / 2 : per) + npair - 1) / npair;
+  const unsigned lg = ordered ? 8u * nwg : nwg;
+  const dim3 g(lg), blk(npair * L * kWave);
   const bool r9 = np == 9 && radius == 3;  // DPVO: p = 3, R = 3
-#define LVL_LAUNCH(TT, RG, R9)                                                                \
-  hipLaunchKernelGGL((corr_nhwc_lvl_kernel<TT, RG, R9>), g, blk, lsm, st, (const TT*)fmap1, lv, L, \
-                     coords, ii, jj, B, M, np, N1, N2, radius, ord, out)
+#define LVL_LAUNCH(TT, R9, PR)                                                                \
+  hipLaunchKernelGGL((corr_nhwc_lvl_kernel<TT, 2, R9, PR>), g, blk, lsm, st, (const TT*)fmap1, lv, \
+                     L, coords, ii, jj, B, M, np, N1, N2, radius, ord, out)
+#define LVL_LAUNCH_P(TT, R9)              \
+  if (corr_lvl_paired(L)) LVL_LAUNCH(TT, R9, true); \
+  else LVL_LAUNCH(TT, R9, false)
   if (dtype == DPVO_F32) {
-    if (r9) LVL_LAUNCH(float, 2, true); else LVL_LAUNCH(float, 2, false);
+    if (r9) { LVL_LAUNCH_P(float, true); } else { LVL_LAUNCH_P(float, false); }
   } else {
-    if (r9) LVL_LAUNCH(__half, 2, true); else LVL_LAUNCH(__half, 2, false);
+    if (r9) { LVL_LAUNCH_P(__half, true); } else { LVL_LAUNCH_P(__half, false); }
   }
+#undef LVL_LAUNCH_P
 #undef LVL_LAUNCH
   return launch_status();
 }

@@ -17,6 +17,11 @@ sys.path.insert(0, REPO)
 
 import torch  # noqa: E402
 
+import dpvo_amd._native as _nat  # noqa: E402
+
+if "--native" in sys.argv:  # A/B: extension modules from another build directory
+    _nat.NATIVE_DIR = os.path.abspath(sys.argv[sys.argv.index("--native") + 1])
+
 from dpvo_amd import altcorr, fastba, synthetic  # noqa: E402
 
 
@@ -39,6 +44,7 @@ def timed(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--native", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     from dpvo_amd.altcorr.correlation import cuda_corr as cc
