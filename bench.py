@@ -42,7 +42,7 @@ TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)),
 
 
 def pmc_traffic(config):
-    """Per-launch HBM bytes of corr_nhwc_kernel from the committed PMC passes
+    """Per-launch HBM bytes of corr_nhwc_lvl_kernel from the committed PMC passes
     (scripts/pmc.sh + scripts/traffic_summary.py; FETCH_SIZE doubled per the
     gfx950 correction). Counters cannot be read live inside the timed run, so
     the figure is only reported for the default cfg2 workload it was taken on."""
@@ -545,10 +545,9 @@ def main():
                 "parallelism": f"replicas x{world}",
             },
             "roofline": {
-                "kernel": ("corr_nhwc_lvl_kernel (A-CORR, all levels, one launch, one wave per "
-                           "(edge, level))" if args.features == "f32" else
-                           "corr_nhwc_kernel (A-CORR, all levels, one launch)"),
-                # how the fp32 products are formed
+                "kernel": "corr_nhwc_lvl_kernel (A-CORR, all levels, one launch, one wave per "
+                          "(edge, level))",
+                # how the products are formed (exact fp32 for fp32 features)
                 "products": ("fp32 x fp32 on v_mfma_f32_16x16x4_f32 (IEEE fp32 products), fp32 "
                              "accumulation"
                              if args.features == "f32" else
