@@ -17,6 +17,7 @@
 #   probe      host enqueue time per call of a step, first after a sync vs steady
 #   stale      the stale-granule regression test; staledemo: its A/B on the round-4 tree
 #   launchprof rocprof kernel durations of the fused start-of-update launch and its parts
+#   launchtrace per-workgroup timeline of that launch inside the bench step (scripts/launch_trace.py)
 #   corrvar    A-CORR product kernel times, fp32 and fp16 (scripts/corr_variants.py)
 #   corrab     A/B of builds copied to scratch_ab/<v> (VARIANTS, scripts/corr_ab.sh)
 #   dropin     per-level NCHW / channels-last drop-in calls (scripts/corr_dropin_bench.py)
@@ -75,6 +76,7 @@ for s in "$@"; do
         -- python scripts/reproject_launch_bench.py cfg2 dpvo25
       python scripts/kstats.py "$(find $O/${T}_launchprof -name '*kernel_stats.csv' | head -1)" 12 \
         | tee $O/${T}_launchprof_kstats.txt ;;
+    launchtrace) run launchtrace 200 python -u scripts/launch_trace.py ;;
     corrvar) run corrvar 200 python -u scripts/corr_variants.py ${CORRVAR_ARGS:-} ;;
     corrpmc) run corrpmc 700 bash scripts/pmc_corrvar.sh ;;
     corrab) run corrab 400 bash scripts/corr_ab.sh ;;
