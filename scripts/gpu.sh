@@ -22,6 +22,7 @@
 #   corrab     A/B of builds copied to scratch_ab/<v> (VARIANTS, scripts/corr_ab.sh)
 #   dropin     per-level NCHW / channels-last drop-in calls (scripts/corr_dropin_bench.py)
 #   benchf16   bench.py --features f16 (the fork's MIXED_PRECISION rings)
+#   spdbench   training-path dense solve vs torch/rocSOLVER (scripts/spd_solve_bench.py)
 #   dpvoprof   rocprofv3 over the fork's live BA call at E = 9850 (scripts/dpvo_window_call.py)
 #   corrpmc    SQ / TCC counter passes over scripts/corr_variants.py (scripts/pmc_corrvar.sh)
 #   corrwide   the channels-last corr tests incl. the wide-dynamic-range ones
@@ -76,6 +77,7 @@ for s in "$@"; do
         -- python scripts/reproject_launch_bench.py cfg2 dpvo25
       python scripts/kstats.py "$(find $O/${T}_launchprof -name '*kernel_stats.csv' | head -1)" 12 \
         | tee $O/${T}_launchprof_kstats.txt ;;
+    spdbench) run spdbench 200 python -u scripts/spd_solve_bench.py ;;
     launchtrace) run launchtrace 200 python -u scripts/launch_trace.py ;;
     corrvar) run corrvar 200 python -u scripts/corr_variants.py ${CORRVAR_ARGS:-} ;;
     corrpmc) run corrpmc 700 bash scripts/pmc_corrvar.sh ;;
