@@ -11,8 +11,12 @@
 //           the lower triangle of H, cholesky_ex default upper=False):
 //           column j: pivot d = a_jj (d <= 0 or NaN: info = j + 1, the
 //           first failed column, as LAPACK potrf), l_jj = sqrt(d),
-//           l_ij = a_ij / l_jj, then a_ic -= l_ij l_cj (j < c <= i);
-//   solve:  L Y = B (forward), L^T X = Y (backward), k right-hand sides.
+//           l_ij = a_ij / l_jj into a contiguous LDS column, then
+//           a_ic -= l_ij l_cj (j < c <= i) by 8 row groups x 32 column lanes;
+//   solve:  L Y = B (forward), L^T X = Y (backward), k right-hand sides;
+//           with one rhs and the factor in LDS, the factor also mirrors L^T
+//           into the upper triangle and wave 0 runs both sweeps alone as
+//           contiguous row axpys (no workgroup barrier per step).
 // Outputs: L (lower, zeros above, like cholesky_ex), X, info.  A failed
 // factorisation leaves X = 0 (the caller's "don't crash training" branch
 // returns zeros anyway).  Deterministic: every sum in a fixed order.
@@ -31,10 +35,14 @@ __device__ __forceinline__ float spd_sqrt<float>(float v) { return sqrtf(v); }
 template <>
 __device__ __forceinline__ double spd_sqrt<double>(double v) { return sqrt(v); }
 
-// M: the n x n working matrix (row-major, LDS or HBM), Y: n x k right-hand sides
+// M: the n x n working matrix (row-major, LDS or HBM), lv: n scratch entries
+// of LDS (the current column), Y: n x k right-hand sides.  Per column: the
+// scaled column goes to lv (contiguous, read as broadcasts and unit-stride
+// runs), then the trailing triangle a_ic -= l_i l_c with 8 row groups x 32
+// column lanes (consecutive c in consecutive lanes); two barriers a column.
 template <typename T>
-__device__ void spd_factor(T* M, int n, int* fail_col) {
-  const int tid = threadIdx.x;
+__device__ void spd_factor(T* M, T* lv, int n, int* fail_col, bool mirror) {
+  const int tid = threadIdx.x, tr = tid >> 5, tc = tid & 31;
   for (int j = 0; j < n; j++) {
     const T d = M[(size_t)j * n + j];
     if (!(d > T(0))) {  // not positive definite (NaN included): block-uniform
@@ -43,22 +51,44 @@ __device__ void spd_factor(T* M, int n, int* fail_col) {
       return;
     }
     const T s = spd_sqrt(d), rs = T(1) / s;
-    // column j below the pivot (each thread its own rows: no barrier needed
-    // between the scale and the diagonal store)
-    for (int i = j + 1 + tid; i < n; i += kSpdThreads) M[(size_t)i * n + j] *= rs;
+    for (int i = j + 1 + tid; i < n; i += kSpdThreads) {
+      const T l = M[(size_t)i * n + j] * rs;
+      M[(size_t)i * n + j] = l;
+      lv[i] = l;
+      if (mirror) M[(size_t)j * n + i] = l;  // L^T in the upper triangle (row j)
+    }
     if (tid == 0) M[(size_t)j * n + j] = s;
     __syncthreads();
-    // trailing lower triangle: pairs (i, c), j < c <= i < n
-    const int m = n - j - 1;
-    const int pairs = m * (m + 1) / 2;
-    for (int p = tid; p < pairs; p += kSpdThreads) {
-      int r = (int)((sqrtf(8.0f * p + 1.0f) - 1.0f) * 0.5f);
-      while (r * (r + 1) / 2 > p) r--;
-      while ((r + 1) * (r + 2) / 2 <= p) r++;
-      const int i = j + 1 + r, c = j + 1 + (p - r * (r + 1) / 2);
-      M[(size_t)i * n + c] -= M[(size_t)i * n + j] * M[(size_t)c * n + j];
+    for (int i = j + 1 + tr; i < n; i += kSpdThreads / 32) {
+      const T li = lv[i];
+      T* row = M + (size_t)i * n;
+      for (int c = j + 1 + tc; c <= i; c += 32) row[c] -= li * lv[c];
     }
     __syncthreads();
+  }
+}
+
+// One right-hand side, L in the lower AND L^T in the upper triangle of M
+// (spd_factor with mirror): both sweeps as column axpys on wave 0 alone, each
+// step reading one contiguous row of M (forward: row j of the upper part =
+// column j of L; backward: row j of L), no workgroup barrier inside a sweep
+// (a wave's LDS accesses complete in order; wave_lds_sync orders the steps).
+template <typename T>
+__device__ void spd_solve1_wave(const T* M, T* y, int n) {
+  const int lane = threadIdx.x;
+  for (int j = 0; j < n; j++) {  // L y = b
+    const T yj = y[j] / M[(size_t)j * n + j];
+    const T* row = M + (size_t)j * n;
+    for (int i = j + 1 + lane; i < n; i += kWave) y[i] -= row[i] * yj;
+    if (lane == 0) y[j] = yj;
+    wave_lds_sync();
+  }
+  for (int j = n - 1; j >= 0; j--) {  // L^T x = y
+    const T xj = y[j] / M[(size_t)j * n + j];
+    const T* row = M + (size_t)j * n;
+    for (int i = lane; i < j; i += kWave) y[i] -= row[i] * xj;
+    if (lane == 0) y[j] = xj;
+    wave_lds_sync();
   }
 }
 
@@ -96,6 +126,7 @@ __global__ void __launch_bounds__(kSpdThreads)
                T* __restrict__ X, int* __restrict__ info, int n, int k, int factor, int in_lds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int fail_col;
+  T* lv = reinterpret_cast<T*>(smem) + (in_lds ? (size_t)n * n + (size_t)n * k : 0);  // [n]
   const int tid = threadIdx.x;
   const size_t b = blockIdx.x, nn = (size_t)n * n, nk = (size_t)n * k;
   const T* Hb = H + b * nn;
@@ -114,12 +145,23 @@ __global__ void __launch_bounds__(kSpdThreads)
     }
   for (size_t e = tid; e < nk; e += kSpdThreads) Y[e] = B[b * nk + e];
   __syncthreads();
-  if (factor) spd_factor(M, n, &fail_col);
+  // one rhs with the factor in LDS: single-wave sweeps over a mirrored factor
+  const bool wave_solve = factor && in_lds && k == 1;
+  if (factor) spd_factor(M, lv, n, &fail_col, wave_solve);
   const bool ok = fail_col == 0;
-  if (ok) spd_solve(M, Y, n, k);
+  if (ok) {
+    if (wave_solve) {
+      if (tid < kWave) spd_solve1_wave(M, Y, n);
+    } else {
+      spd_solve(M, Y, n, k);
+    }
+  }
   __syncthreads();
   if (factor && in_lds && Lb)  // (in HBM the factor is already in place, zeros above)
-    for (size_t e = tid; e < nn; e += kSpdThreads) Lb[e] = M[e];
+    for (size_t e = tid; e < nn; e += kSpdThreads) {
+      const int i = (int)(e / n), c = (int)(e % n);
+      Lb[e] = c <= i ? M[e] : T(0);  // the mirrored upper triangle is not part of L
+    }
   for (size_t e = tid; e < nk; e += kSpdThreads) Xb[e] = ok ? Y[e] : T(0);
   if (tid == 0 && info) info[b] = fail_col;
 }
@@ -127,9 +169,12 @@ __global__ void __launch_bounds__(kSpdThreads)
 template <typename T>
 int spd_launch(const void* H, const void* B, void* L, void* X, int32_t* info, int batch, int n,
                int k, int factor, void* stream) {
-  const size_t lds = sizeof(T) * ((size_t)n * n + (size_t)n * k);
-  const int in_lds = lds <= kSpdLds - 64;
+  // LDS: matrix + right-hand sides (when they fit) + the column scratch lv[n]
+  const size_t full = sizeof(T) * ((size_t)n * n + (size_t)n * k + (size_t)n);
+  const int in_lds = full <= kSpdLds - 64;
+  const size_t lds = in_lds ? full : sizeof(T) * (size_t)n;
   if (!in_lds && factor && !L) return DPVO_ERR_INVALID;  // the HBM working copy is the factor buffer
+  if (!in_lds && lds > 64 * 1024) return DPVO_ERR_UNSUPPORTED;  // lv alone past 64 KB: n > 8192
   if (in_lds && lds > 64 * 1024) {
     // the dynamic LDS beyond the default 64 KB (the static fail flag sits on
     // top), set once per device and instantiation
@@ -145,7 +190,7 @@ int spd_launch(const void* H, const void* B, void* L, void* X, int32_t* info, in
       attr_set[dev] = true;
     }
   }
-  hipLaunchKernelGGL(spd_kernel<T>, dim3(batch), dim3(kSpdThreads), in_lds ? lds : 0,
+  hipLaunchKernelGGL(spd_kernel<T>, dim3(batch), dim3(kSpdThreads), lds,
                      as_stream(stream), (const T*)H, (const T*)B, (T*)L, (T*)X, (int*)info, n, k,
                      factor, in_lds);
   return launch_status();
