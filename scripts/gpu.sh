@@ -13,6 +13,7 @@
 #   bench      bench.py $BENCH_ARGS (full default run, CPU baseline included)
 #   prof       rocprofv3 --kernel-trace --stats over a 200-step bench (kernel table printed)
 #   profdrv    the same over the driver's 20-step command
+#   proff16    the same over a 200-step bench with fp16 features
 #   phases     BA window phase tables: cfg2 2 iterations, DPVO windows E=9850 / 3940 1 iteration
 #   probe      host enqueue time per call of a step, first after a sync vs steady
 #   stale      the stale-granule regression test; staledemo: its A/B on the round-4 tree
@@ -65,6 +66,7 @@ for s in "$@"; do
     bench) run bench 400 python -u bench.py ${BENCH_ARGS:-} ;;
     prof) prof prof --steps 200 --warmup 10 ;;
     profdrv) prof profdrv --steps 20 --warmup 5 ;;
+    proff16) prof proff16 --steps 200 --warmup 10 --features f16 ;;
     phases)
       run phases_cfg2 300 python -u scripts/ba_window_phases.py cfg2 2
       run phases_dpvo25_1 300 python -u scripts/ba_window_phases.py 25 1
